@@ -1,0 +1,183 @@
+"""Pin the CPU oracle (oracle/) against the committed golden fixtures.
+
+The fixtures were produced by tests/golden/make_golden.py from hashlib,
+libsodium 1.0.18 and a pure-Python textbook model -- none of which share code
+with oracle/.  These tests run on CPU only.
+"""
+import hashlib
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from _oracle import expand
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _json(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+# ---------------------------------------------------------------- SHA-512
+def test_sha512_vectors(oracle):
+    v = _json("sha512_vectors.json")
+    for e in v["vectors"]:
+        m = expand(e["label"].encode(), e["len"])
+        assert oracle.sha512(m).hex() == e["digest512"], e["len"]
+
+
+def test_sha512_reference_fixtures(oracle):
+    ref = _json("sha512_vectors.json")["reference_fixtures"]
+    # worker/src/tests/processor_tests.rs:9-46 -- Processor digest of the 228-B batch
+    b = bytes.fromhex(ref["processor_batch_228B"]["hex"])
+    assert len(b) == 228
+    assert oracle.digest(b).hex() == ref["processor_batch_228B"]["digest32"]
+    assert ref["processor_batch_228B"]["digest32"].startswith("24d00f74a0767e74")
+    assert oracle.digest(b"Hello, world!").hex() == ref["hello_world"]["digest32"]
+    # a real 508,052-B sealed batch and a 500,000-B buffer (config 1)
+    rb = ref["real_batch_977x512"]
+    txs = [expand((rb["tx_label"] % i).encode(), rb["tx_len"]) for i in range(rb["ntx"])]
+    real = struct.pack("<IQ", 0, len(txs)) + b"".join(struct.pack("<Q", len(t)) + t for t in txs)
+    assert len(real) == rb["len"] == 508052
+    assert oracle.digest(real).hex() == rb["digest32"]
+    buf = expand(ref["buffer_500000"]["label"].encode(), 500000)
+    assert oracle.digest(buf).hex() == ref["buffer_500000"]["digest32"]
+
+
+def test_sha512_many_threads(oracle):
+    rng = np.random.default_rng(7)
+    lens = rng.integers(0, 3000, size=257).astype(np.uint64)
+    off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    data = rng.integers(0, 256, size=int(lens.sum()) + 1, dtype=np.uint8)
+    out = oracle.sha512_trunc32_many(data, off, lens, nthreads=4)
+    for i in range(len(lens)):
+        m = data[int(off[i]):int(off[i] + lens[i])].tobytes()
+        assert out[i].tobytes() == hashlib.sha512(m).digest()[:32]
+
+
+# ---------------------------------------------------------------- fixture keys
+def test_chacha20_rfc7539_zero_key(oracle):
+    # RFC 7539 §2.3.2-style known answer for key = 0, nonce = 0, counter = 0
+    ks = oracle.chacha20(bytes(32), 64)
+    assert ks[:16].hex() == "76b8e0ada0f13d90405d6ae55386bd28"
+
+
+def test_keys_fixture(oracle):
+    ref = _json("fixtures_reference.json")
+    ks = oracle.chacha20(bytes(32), 128)
+    for i, k in enumerate(ref["keys"]):
+        seed = ks[32 * i:32 * i + 32]
+        assert seed.hex() == k["seed"]
+        assert oracle.pubkey(seed).hex() == k["pk"]
+
+
+def test_sign_matches_libsodium(oracle):
+    ref = _json("fixtures_reference.json")
+    d = bytes.fromhex(ref["hello_digest"])
+    for k, s in zip(ref["keys"], ref["hello_signatures"]):
+        seed, pk = bytes.fromhex(k["seed"]), bytes.fromhex(k["pk"])
+        assert oracle.sign(seed, pk, d).hex() == s
+
+
+# ---------------------------------------------------------------- reference crypto_tests.rs
+def _kp(ref, i):
+    return bytes.fromhex(ref["keys"][i]["seed"]), bytes.fromhex(ref["keys"][i]["pk"])
+
+
+def test_verify_valid_signature(oracle):            # crypto_tests.rs:49-61
+    ref = _json("fixtures_reference.json")
+    seed, pk = _kp(ref, 3)
+    d = oracle.digest(b"Hello, world!")
+    assert oracle.verify_strict(pk, oracle.sign(seed, pk, d), d)
+
+
+def test_verify_invalid_signature(oracle):          # crypto_tests.rs:63-77
+    ref = _json("fixtures_reference.json")
+    seed, pk = _kp(ref, 3)
+    sig = oracle.sign(seed, pk, oracle.digest(b"Hello, world!"))
+    assert not oracle.verify_strict(pk, sig, oracle.digest(b"Bad message!"))
+
+
+def test_verify_valid_batch(oracle):                # crypto_tests.rs:79-94
+    ref = _json("fixtures_reference.json")
+    d = oracle.digest(b"Hello, world!")
+    pks, sigs = [], []
+    for i in (3, 2, 1):
+        seed, pk = _kp(ref, i)
+        pks.append(pk)
+        sigs.append(oracle.sign(seed, pk, d))
+    assert oracle.verify_batch(pks, sigs, d)
+
+
+def test_verify_invalid_batch(oracle):              # crypto_tests.rs:96-115
+    ref = _json("fixtures_reference.json")
+    d = oracle.digest(b"Hello, world!")
+    pks, sigs = [], []
+    for i in (3, 2):
+        seed, pk = _kp(ref, i)
+        pks.append(pk)
+        sigs.append(oracle.sign(seed, pk, d))
+    pks.append(_kp(ref, 1)[1])
+    sigs.append(bytes(64))  # Signature::default()
+    assert not oracle.verify_batch(pks, sigs, d)
+
+
+def test_verify_batch_empty(oracle):
+    assert oracle.verify_batch([], [], bytes(32))
+
+
+# ---------------------------------------------------------------- edge-case corpus
+@pytest.fixture(scope="module")
+def corpus():
+    d = np.load(os.path.join(GOLD, "ed25519_corpus.npz"))
+    return {k: d[k] for k in d.files}
+
+
+def _entry(c, i):
+    o, n = int(c["off"][i]), int(c["len"][i])
+    return c["pk"][i].tobytes(), c["sig"][i].tobytes(), c["msg"][o:o + n].tobytes()
+
+
+def test_corpus_verify_strict(oracle, corpus):
+    meta = _json("ed25519_corpus.json")
+    for i in range(len(corpus["cat"])):
+        pk, sig, m = _entry(corpus, i)
+        got = oracle.verify_strict(pk, sig, m)
+        assert got == bool(corpus["strict"][i]), (i, meta["categories"][corpus["cat"][i]])
+        assert got == bool(corpus["sodium"][i])
+
+
+def test_corpus_batch_rule_and_class(oracle, corpus):
+    for i in range(len(corpus["cat"])):
+        pk, sig, m = _entry(corpus, i)
+        assert oracle.verify_cofactorless(pk, sig, m) == bool(corpus["batch_rule"][i]), i
+        assert oracle.verify_batch([pk], [sig], m) == bool(corpus["batch_rule"][i]), i
+        assert oracle.batch_class(pk, sig, m) == int(corpus["batch_class"][i]), i
+
+
+def test_corpus_bulk_threads(oracle, corpus):
+    got = oracle.verify_strict_many(corpus["pk"], corpus["sig"], corpus["msg"], corpus["off"],
+                                    corpus["len"], nthreads=4)
+    assert np.array_equal(got, corpus["strict"])
+
+
+def test_batch_groups_fixture(oracle):
+    g = np.load(os.path.join(GOLD, "batch_groups.npz"))
+    gb, sb = oracle.verify_batch_groups(g["pk"], g["sig"], g["first"], g["cnt"], g["msg32"], nthreads=3)
+    assert np.array_equal(gb, g["expect"])
+    # per-signature bits AND to the group bit
+    for i in range(len(g["cnt"])):
+        f, c = int(g["first"][i]), int(g["cnt"][i])
+        assert bool(gb[i]) == bool(np.all(sb[f:f + c]))
+
+
+def test_torsion_points(oracle):
+    meta = _json("ed25519_corpus.json")
+    mine = sorted(oracle.torsion_point(i).hex() for i in range(8))
+    assert mine == sorted(meta["torsion_encodings"])
+    for e in meta["small_order_encodings"]:
+        assert oracle.point_is_small_order(bytes.fromhex(e))
