@@ -1,0 +1,116 @@
+/*
+ * ntcrypto.h -- C ABI of the MI355X (gfx950) crypto backend for Narwhal/Tusk.
+ *
+ * Drop-in boundary: the reference's `crypto` crate (crypto/src/lib.rs) keeps
+ * its public Rust surface; its FFI binds these symbols.
+ *
+ *   nt_sha512_trunc32            replaces  Digest(Sha512::digest(&batch)[..32])
+ *                                          worker/src/processor.rs:38,
+ *                                          worker/src/batch_maker.rs:124-128 (benchmark hash),
+ *                                          primary/src/messages.rs:70-84 (Header::digest),
+ *                                          :145-153 (Vote::digest), :226-234 (Certificate::digest)
+ *   nt_ed25519_verify_strict     replaces  Signature::verify -> dalek verify_strict
+ *                                          crypto/src/lib.rs:200-204
+ *   nt_ed25519_verify_batch_groups replaces Signature::verify_batch -> dalek verify_batch
+ *                                          crypto/src/lib.rs:206-219, called once per
+ *                                          certificate by Certificate::verify
+ *                                          primary/src/messages.rs:189-215
+ *   nt_ed25519_sign_batch /      batch form of Signature::new / generate_keypair
+ *   nt_ed25519_keypair_batch               crypto/src/lib.rs:163-191 (NOT constant time:
+ *                                          corpus generation and tests only)
+ *
+ * Conventions
+ *   - Host entry points take caller-owned host memory, borrowed for the call;
+ *     the library stages it into its own device buffers and keeps no pointer.
+ *   - Calls are synchronous.  Verdicts are data (bitmaps), never errors.
+ *   - Bitmaps: bit i of byte i/8 (LSB first) = item i; 1 = accept.
+ *   - Return 0 on success, < 0 on failure (NT_E*).  A caller must never turn a
+ *     negative return into "reject"; there is NO CPU fallback inside this
+ *     library: without a usable gfx950 device nt_init fails with NT_ENODEV.
+ *   - Thread-safe: calls on one context may come from several threads; work
+ *     on each device is serialized by a per-device lock.
+ *   - Multi-GPU: host entry points shard items by contiguous index ranges
+ *     over the context's devices (certificates are never split); no
+ *     collective, results gathered on the host.
+ *   - nt_dev_* entry points take DEVICE pointers on device `dev` of the
+ *     context and a hipStream_t (NULL = the library's stream), and only
+ *     enqueue work.  Word-typed buffers (pk, sig, seed, out) must be 16-byte
+ *     aligned; message data may have any alignment.
+ */
+#ifndef NTCRYPTO_H
+#define NTCRYPTO_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NT_OK 0
+#define NT_EINVAL (-1)
+#define NT_EHIP (-2)
+#define NT_ENOMEM (-3)
+#define NT_ENODEV (-4)
+
+#define NT_MODE_STRICT 0       /* dalek verify_strict */
+#define NT_MODE_COFACTORLESS 1 /* per-entry rule of dalek verify_batch */
+
+typedef struct nt_ctx nt_ctx;
+
+/* num_gpus: 0 = all visible devices, k > 0 = the first k, -1 = CPU only
+ * (unsupported: returns NT_ENODEV -- this library has no CPU path). */
+int nt_init(nt_ctx **out, int num_gpus);
+/* One specific device ordinal (used by one-process-per-GPU launchers). */
+int nt_init_device(nt_ctx **out, int device_ordinal);
+void nt_free(nt_ctx *ctx);
+int nt_num_devices(const nt_ctx *ctx);
+const char *nt_strerror(int code);
+/* Library / build identification, e.g. "ntcrypto 0.1 gfx950". */
+const char *nt_version(void);
+
+/* SHA-512 truncated to 32 bytes of n independent messages packed in `data`
+ * (message i = data[off[i] .. off[i] + len[i])).  out32: n * 32 bytes. */
+int nt_sha512_trunc32(nt_ctx *ctx, const uint8_t *data, const uint64_t *off, const uint64_t *len,
+                      uint64_t n, uint8_t *out32);
+
+/* dalek verify_strict for n (pk, sig, msg) triples.  pk32: n*32, sig64: n*64 (R || s),
+ * message i = msg[off[i] .. off[i] + len[i]).  out_bitmap: ceil(n/8) bytes. */
+int nt_ed25519_verify_strict(nt_ctx *ctx, const uint8_t *pk32, const uint8_t *sig64,
+                             const uint8_t *msg, const uint64_t *off, const uint64_t *len,
+                             uint64_t n, uint8_t *out_bitmap);
+
+/* Narwhal verify_batch semantics for G certificates at once: group g has cnt[g]
+ * (pk, sig) pairs starting at index first[g], all over the 32-byte msg32[g].
+ * out_group_bitmap: ceil(G/8) bytes; out_sig_bitmap (nullable): one bit per
+ * pair, sized for max(first[g] + cnt[g]) pairs.  Empty group -> accept. */
+int nt_ed25519_verify_batch_groups(nt_ctx *ctx, const uint8_t *pk32, const uint8_t *sig64,
+                                   const uint64_t *first, const uint32_t *cnt,
+                                   const uint8_t *msg32, uint64_t G, uint8_t *out_group_bitmap,
+                                   uint8_t *out_sig_bitmap);
+
+/* Keygen (seed -> pk) and RFC 8032 signing of message i with seed i.
+ * sig64 may be NULL (keygen only).  Not constant time. */
+int nt_ed25519_sign_batch(nt_ctx *ctx, const uint8_t *seed32, const uint8_t *msg,
+                          const uint64_t *off, const uint64_t *len, uint64_t n, uint8_t *pk32,
+                          uint8_t *sig64);
+int nt_ed25519_keypair_batch(nt_ctx *ctx, const uint8_t *seed32, uint64_t n, uint8_t *pk32);
+
+/* ---- device-resident entry points (enqueue only) ---------------------- */
+int nt_dev_sha512_trunc32(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_data,
+                          const uint64_t *d_off, const uint64_t *d_len, uint64_t n,
+                          uint8_t *d_out32);
+/* d_out_words: ceil(n/64) little-endian 64-bit bitmap words. */
+int nt_dev_ed25519_verify(nt_ctx *ctx, int dev, void *stream, int mode, const uint8_t *d_pk32,
+                          const uint8_t *d_sig64, const uint8_t *d_msg, const uint64_t *d_off,
+                          const uint64_t *d_len, uint64_t n, uint64_t *d_out_words);
+int nt_dev_group_and(nt_ctx *ctx, int dev, void *stream, const uint64_t *d_first,
+                     const uint32_t *d_cnt, uint64_t G, const uint64_t *d_sig_words,
+                     uint64_t *d_group_words);
+int nt_dev_ed25519_sign(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_seed32,
+                        const uint8_t *d_msg, const uint64_t *d_off, const uint64_t *d_len,
+                        uint64_t n, uint8_t *d_pk32, uint8_t *d_sig64);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NTCRYPTO_H */

@@ -1,0 +1,466 @@
+// kernels.hip -- gfx950 kernels of the Narwhal/Tusk crypto hot path.
+//
+//   k_sha512_trunc32      one lane per message, Digest = SHA-512[..32]
+//                         (worker/src/processor.rs:38; primary/src/messages.rs:70-84,145-153,226-234)
+//   k_ed25519_verify<M>   one lane per signature; M = strict (crypto/src/lib.rs:200-204 ->
+//                         dalek verify_strict) or cofactorless (per-entry rule of
+//                         crypto/src/lib.rs:206-219 -> dalek verify_batch);
+//                         writes one verdict bit per signature (64-bit ballot words)
+//   k_group_and           AND of per-signature bits over each certificate's vote range
+//   k_ed25519_sign        keygen + RFC 8032 signing (corpus generation / SignatureService
+//                         batch form; crypto/src/lib.rs:163-191) -- not constant time
+//   k_btab_init           [j]B, j = 0..128, affine-niels table (built once per device)
+//
+// SIMT design: every lane runs the same window schedule (fixed signed windows,
+// never per-lane sliding windows), so lanes of a wave never diverge inside the
+// double-scalar ladder.  [s]B uses 8-bit windows over a 129-entry affine table
+// staged in LDS (16.5 KiB per workgroup); [k](-A) uses 4-bit windows over a
+// per-lane 9-entry cached table in a global workspace laid out lane-minor so
+// each lane's 16-byte accesses coalesce across the workgroup.
+#include <hip/hip_runtime.h>
+
+#include "fe25519.hpp"
+#include "ge25519.hpp"
+#include "kernels.hpp"
+#include "sc25519.hpp"
+#include "sha512.hpp"
+
+namespace nt {
+
+constexpr int kBlock = 256;
+constexpr int kBEntries = 129;        // |digit| in 0..128
+constexpr int kBStride = 32;          // words per niels entry (30 used)
+constexpr int kAEntries = 9;          // |digit| in 0..8
+constexpr int kAQuads = 10;           // uint4 per cached entry (40 words)
+
+// --------------------------------------------------------------------------
+// SHA-512 digests
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_sha512_trunc32(const uint8_t* __restrict__ data,
+                                                          const uint64_t* __restrict__ off,
+                                                          const uint64_t* __restrict__ len,
+                                                          uint64_t n, uint32_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  uint64_t st[8];
+  sha512_prefixed<0>(st, nullptr, data + off[i], len[i]);
+  uint32_t w[8];
+  sha512_out_words(w, st, 8);
+  uint4* o = (uint4*)(out + 8 * i);
+  o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+// --------------------------------------------------------------------------
+// Base-point table
+// --------------------------------------------------------------------------
+NT_D NT_INLINE void store_niels(uint32_t* dst, const ge_niels& q) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    dst[i] = q.ypx.v[i];
+    dst[10 + i] = q.ymx.v[i];
+    dst[20 + i] = q.xy2d.v[i];
+  }
+  dst[30] = 0;
+  dst[31] = 0;
+}
+
+__global__ void k_btab_init(uint32_t* __restrict__ tab) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= kBEntries) return;
+  ge_niels q;
+  if (j == 0) {
+    ge_niels_0(q);
+    store_niels(tab, q);
+    return;
+  }
+  uint32_t enc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) enc[i] = kBaseEnc[i];
+  ge_p3 B, P;
+  ge_frombytes_w(B, enc);
+  ge_cached Bc;
+  ge_p3_to_cached(Bc, B);
+  ge_p3_0(P);
+  for (int bit = 7; bit >= 0; --bit) {
+    ge_p2 t2;
+    ge_cp t;
+    ge_p3_to_p2(t2, P);
+    ge_dbl(t, t2);
+    ge_cp_to_p3(P, t);
+    if ((j >> bit) & 1) {
+      ge_add_cached(t, P, Bc);
+      ge_cp_to_p3(P, t);
+    }
+  }
+  fe zi, x, y, d2;
+  fe_invert(zi, P.Z);
+  fe_mul(x, P.X, zi);
+  fe_mul(y, P.Y, zi);
+  fe_add(q.ypx, y, x);
+  fe_carry(q.ypx);
+  fe_sub(q.ymx, y, x);
+  fe_carry(q.ymx);
+  fe_const(d2, kFeD2);
+  fe_mul(q.xy2d, x, y);
+  fe_mul(q.xy2d, q.xy2d, d2);
+  store_niels(tab + (size_t)j * kBStride, q);
+}
+
+// --------------------------------------------------------------------------
+// Table access helpers
+// --------------------------------------------------------------------------
+NT_D NT_INLINE void lds_load_niels(ge_niels& q, const uint32_t* btab, uint32_t idx) {
+  const uint4* e = (const uint4*)(btab + idx * kBStride);
+  uint32_t w[32];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint4 v = e[i];
+    w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    q.ypx.v[i] = w[i];
+    q.ymx.v[i] = w[10 + i];
+    q.xy2d.v[i] = w[20 + i];
+  }
+}
+
+// workspace: [slot][entry][quad][lane] of uint4
+NT_D NT_INLINE void ws_store_cached(uint4* ws, uint32_t slot, uint32_t entry, const ge_cached& c) {
+  uint32_t w[40];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    w[i] = c.YpX.v[i]; w[10 + i] = c.YmX.v[i]; w[20 + i] = c.Z2.v[i]; w[30 + i] = c.T2d.v[i];
+  }
+  uint4* base = ws + ((size_t)(slot * kAEntries + entry) * kAQuads) * kBlock + threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < kAQuads; ++q)
+    base[(size_t)q * kBlock] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
+NT_D NT_INLINE void ws_load_cached(ge_cached& c, const uint4* ws, uint32_t slot, uint32_t entry) {
+  uint32_t w[40];
+  const uint4* base = ws + ((size_t)(slot * kAEntries + entry) * kAQuads) * kBlock + threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < kAQuads; ++q) {
+    const uint4 v = base[(size_t)q * kBlock];
+    w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    c.YpX.v[i] = w[i]; c.YmX.v[i] = w[10 + i]; c.Z2.v[i] = w[20 + i]; c.T2d.v[i] = w[30 + i];
+  }
+}
+
+NT_D NT_INLINE void load_btab_lds(uint32_t* lds, const uint32_t* __restrict__ btab_g) {
+  const uint4* src = (const uint4*)btab_g;
+  uint4* dst = (uint4*)lds;
+  for (int i = threadIdx.x; i < kBEntries * kBStride / 4; i += kBlock) dst[i] = src[i];
+  __syncthreads();
+}
+
+// --------------------------------------------------------------------------
+// Double-scalar ladder:  acc = [s]B + [k]Aneg   (4-bit k windows, 8-bit s windows)
+// --------------------------------------------------------------------------
+NT_D NT_INLINE void ladder(ge_p2& acc, const uint32_t kd[8], const uint32_t sd[8], const uint4* ws,
+                           uint32_t slot, const uint32_t* btab) {
+  uint32_t kw[8], sw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { kw[i] = kd[i]; sw[i] = sd[i]; }
+  ge_p2_0(acc);
+  ge_cp t;
+  ge_p3 u;
+  for (int wi = 7; wi >= 0; --wi) {
+    const uint32_t kcur = kw[7], scur = sw[7];
+#pragma unroll
+    for (int m = 7; m > 0; --m) { kw[m] = kw[m - 1]; sw[m] = sw[m - 1]; }
+    for (int j = 7; j >= 0; --j) {
+      for (int r = 0; r < 3; ++r) ge_dbl_p2(acc, acc);
+      ge_dbl(t, acc);
+      ge_cp_to_p3(u, t);
+      // k digit: two's-complement nibble
+      const int32_t dk = (int32_t)(((kcur >> (4 * j)) & 15u) ^ 8u) - 8;
+      const uint32_t negk = dk < 0;
+      ge_cached ce;
+      ws_load_cached(ce, ws, slot, (uint32_t)(negk ? -dk : dk));
+      ge_cached_cneg(ce, negk);
+      ge_add_cached(t, u, ce);
+      if ((j & 1) == 0) {
+        const int32_t ds = (int32_t)(((scur >> (4 * j)) & 255u) ^ 128u) - 128;
+        const uint32_t negs = ds < 0;
+        ge_niels ne;
+        lds_load_niels(ne, btab, (uint32_t)(negs ? -ds : ds));
+        ge_niels_cneg(ne, negs);
+        ge_cp_to_p3(u, t);
+        ge_add_niels(t, u, ne);
+      }
+      ge_cp_to_p2(acc, t);
+    }
+  }
+}
+
+// Fixed-base [x]B with 8-bit windows (x < L), used for keygen and signing.
+NT_D NT_INLINE void base_mul(ge_p2& acc, const uint32_t x[8], const uint32_t* btab) {
+  uint32_t sd[8];
+  sc_recode_w8(sd, x);
+  ge_p2_0(acc);
+  ge_cp t;
+  ge_p3 u;
+  for (int wi = 7; wi >= 0; --wi) {
+    const uint32_t scur = sd[7];
+#pragma unroll
+    for (int m = 7; m > 0; --m) sd[m] = sd[m - 1];
+    for (int j = 3; j >= 0; --j) {
+      for (int r = 0; r < 7; ++r) ge_dbl_p2(acc, acc);
+      ge_dbl(t, acc);
+      ge_cp_to_p3(u, t);
+      const int32_t ds = (int32_t)(((scur >> (8 * j)) & 255u) ^ 128u) - 128;
+      const uint32_t negs = ds < 0;
+      ge_niels ne;
+      lds_load_niels(ne, btab, (uint32_t)(negs ? -ds : ds));
+      ge_niels_cneg(ne, negs);
+      ge_add_niels(t, u, ne);
+      ge_cp_to_p2(acc, t);
+    }
+  }
+}
+
+NT_D NT_INLINE void load8(uint32_t w[8], const uint32_t* __restrict__ p) {
+  const uint4* q = (const uint4*)p;
+  const uint4 a = q[0], b = q[1];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+
+// --------------------------------------------------------------------------
+// Verification
+// --------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_ed25519_verify(
+    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t n,
+    const uint32_t* __restrict__ btab_g, uint4* __restrict__ ws,
+    unsigned long long* __restrict__ out_bits) {
+  __shared__ __attribute__((aligned(16))) uint32_t btab[kBEntries * kBStride];
+  load_btab_lds(btab, btab_g);
+  const uint32_t slot = blockIdx.x;
+  for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < n; base += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t gi = base + threadIdx.x;
+    const uint32_t active = gi < n;
+    const uint64_t i = active ? gi : n - 1;
+
+    uint32_t Aw[8], Rw[8], Sw[8];
+    load8(Aw, pk + 8 * i);
+    load8(Rw, sig + 16 * i);
+    load8(Sw, sig + 16 * i + 8);
+
+    const uint32_t s_ok = sc_is_canonical(Sw);
+    ge_p3 A, R;
+    const uint32_t a_ok = ge_frombytes_w(A, Aw);
+    const uint32_t r_ok = ge_frombytes_w(R, Rw);
+    uint32_t small = 0;
+    if (MODE == kStrict) small = ge_is_small_order(A) | ge_is_small_order(R);
+
+    // k = H(R || A || M) mod L over the raw encodings
+    uint32_t prefix[16];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { prefix[q] = Rw[q]; prefix[8 + q] = Aw[q]; }
+    uint64_t st[8];
+    sha512_prefixed<16>(st, prefix, msg + off[i], len[i]);
+    uint32_t hw[16], k[8];
+    sha512_out_words(hw, st, 16);
+    sc_reduce512(k, hw);
+
+    // table of j * (-A), j = 0..8
+    ge_p3 An;
+    fe_neg(An.X, A.X);
+    fe_carry(An.X);
+    An.Y = A.Y;
+    An.Z = A.Z;
+    fe_neg(An.T, A.T);
+    fe_carry(An.T);
+    {
+      ge_cached c0, c1;
+      ge_cached_0(c0);
+      ws_store_cached(ws, slot, 0, c0);
+      ge_p3_to_cached(c1, An);
+      ws_store_cached(ws, slot, 1, c1);
+      ge_p3 cur = An;
+      for (uint32_t j = 2; j < kAEntries; ++j) {
+        ge_cp t;
+        ge_add_cached(t, cur, c1);
+        ge_cp_to_p3(cur, t);
+        ge_cached cj;
+        ge_p3_to_cached(cj, cur);
+        ws_store_cached(ws, slot, j, cj);
+      }
+    }
+
+    uint32_t kd[8], sd[8];
+    sc_recode_w4(kd, k);
+    sc_recode_w8(sd, Sw);
+    ge_p2 Rp;
+    ladder(Rp, kd, sd, ws, slot, btab);
+    const uint32_t eq = ge_eq_affine(Rp, R);
+
+    const uint32_t ok = active & s_ok & a_ok & r_ok & (small ^ 1u) & eq;
+    const unsigned long long bal = __ballot(ok);
+    const uint64_t wbase = base + (threadIdx.x & ~63u);
+    if ((threadIdx.x & 63u) == 0 && wbase < n) out_bits[wbase >> 6] = bal;
+  }
+}
+
+// --------------------------------------------------------------------------
+// Certificate groups: AND of the per-signature bits in [first, first + cnt)
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_group_and(const uint64_t* __restrict__ first,
+                                                     const uint32_t* __restrict__ cnt, uint64_t G,
+                                                     const unsigned long long* __restrict__ sig_bits,
+                                                     unsigned long long* __restrict__ out_bits) {
+  const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  uint32_t ok = 0;
+  if (g < G) {
+    ok = 1;
+    const uint64_t f = first[g];
+    const uint64_t e = f + cnt[g];
+    for (uint64_t x = f; x < e;) {
+      const uint64_t w = x >> 6, sh = x & 63;
+      const uint64_t take = (64 - sh) < (e - x) ? (64 - sh) : (e - x);
+      const unsigned long long m = (take == 64 ? ~0ull : ((1ull << take) - 1)) << sh;
+      ok &= ((sig_bits[w] & m) == m);
+      x += take;
+    }
+  }
+  const unsigned long long bal = __ballot(ok);
+  const uint64_t wbase = (uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u);
+  if ((threadIdx.x & 63u) == 0 && wbase < G) out_bits[wbase >> 6] = bal;
+}
+
+// --------------------------------------------------------------------------
+// Keygen + signing (RFC 8032 / dalek Keypair::sign)
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_ed25519_sign(const uint32_t* __restrict__ seed,
+                                                        const uint8_t* __restrict__ msg,
+                                                        const uint64_t* __restrict__ off,
+                                                        const uint64_t* __restrict__ len, uint64_t n,
+                                                        const uint32_t* __restrict__ btab_g,
+                                                        uint32_t* __restrict__ out_pk,
+                                                        uint32_t* __restrict__ out_sig) {
+  __shared__ __attribute__((aligned(16))) uint32_t btab[kBEntries * kBStride];
+  load_btab_lds(btab, btab_g);
+  for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < n; base += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t gi = base + threadIdx.x;
+    const uint32_t active = gi < n;
+    const uint64_t i = active ? gi : n - 1;
+    uint32_t sw[8];
+    load8(sw, seed + 8 * i);
+    uint64_t st[8];
+    sha512_prefixed<8>(st, sw, nullptr, 0);
+    uint32_t h[16];
+    sha512_out_words(h, st, 16);
+    uint32_t a[8], pre[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { a[q] = h[q]; pre[q] = h[8 + q]; }
+    a[0] &= 0xfffffff8u;
+    a[7] &= 0x3fffffffu;
+    a[7] |= 0x40000000u;
+    uint32_t ared[8];
+    sc_reduce256(ared, a);
+    ge_p2 P;
+    base_mul(P, ared, btab);
+    uint32_t Aw[8];
+    ge_tobytes_w(Aw, P);
+
+    const uint8_t* m = msg ? msg + off[i] : nullptr;
+    const uint64_t ml = msg ? len[i] : 0;
+    sha512_prefixed<8>(st, pre, m, ml);
+    uint32_t hr[16], r[8];
+    sha512_out_words(hr, st, 16);
+    sc_reduce512(r, hr);
+    base_mul(P, r, btab);
+    uint32_t Rw[8];
+    ge_tobytes_w(Rw, P);
+
+    uint32_t prefix[16];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { prefix[q] = Rw[q]; prefix[8 + q] = Aw[q]; }
+    sha512_prefixed<16>(st, prefix, m, ml);
+    uint32_t hk[16], k[8], s[8];
+    sha512_out_words(hk, st, 16);
+    sc_reduce512(k, hk);
+    sc_muladd(s, k, a, r);
+    if (active) {
+      uint4* po = (uint4*)(out_pk + 8 * i);
+      po[0] = make_uint4(Aw[0], Aw[1], Aw[2], Aw[3]);
+      po[1] = make_uint4(Aw[4], Aw[5], Aw[6], Aw[7]);
+      if (out_sig) {
+        uint4* so = (uint4*)(out_sig + 16 * i);
+        so[0] = make_uint4(Rw[0], Rw[1], Rw[2], Rw[3]);
+        so[1] = make_uint4(Rw[4], Rw[5], Rw[6], Rw[7]);
+        so[2] = make_uint4(s[0], s[1], s[2], s[3]);
+        so[3] = make_uint4(s[4], s[5], s[6], s[7]);
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------------------------
+// Launchers (host)
+// --------------------------------------------------------------------------
+hipError_t launch_btab_init(uint32_t* d_tab, hipStream_t s) {
+  hipLaunchKernelGGL(k_btab_init, dim3(3), dim3(64), 0, s, d_tab);
+  return hipGetLastError();
+}
+
+hipError_t launch_sha512_trunc32(const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
+                                 uint64_t n, uint8_t* d_out32, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t blocks = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_sha512_trunc32, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_data, d_off,
+                     d_len, n, (uint32_t*)d_out32);
+  return hipGetLastError();
+}
+
+hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
+                         const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
+                         const uint32_t* d_btab, void* d_ws, uint32_t ws_slots, uint64_t* d_out_words,
+                         hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  uint64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > ws_slots) blocks = ws_slots;
+  if (mode == kStrict)
+    hipLaunchKernelGGL(k_ed25519_verify<kStrict>, dim3((uint32_t)blocks), dim3(kBlock), 0, s,
+                       (const uint32_t*)d_pk, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_btab,
+                       (uint4*)d_ws, (unsigned long long*)d_out_words);
+  else
+    hipLaunchKernelGGL(k_ed25519_verify<kCofactorless>, dim3((uint32_t)blocks), dim3(kBlock), 0, s,
+                       (const uint32_t*)d_pk, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_btab,
+                       (uint4*)d_ws, (unsigned long long*)d_out_words);
+  return hipGetLastError();
+}
+
+hipError_t launch_group_and(const uint64_t* d_first, const uint32_t* d_cnt, uint64_t G,
+                            const uint64_t* d_sig_words, uint64_t* d_group_words, hipStream_t s) {
+  if (G == 0) return hipSuccess;
+  const uint64_t blocks = (G + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_group_and, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_first, d_cnt, G,
+                     (const unsigned long long*)d_sig_words, (unsigned long long*)d_group_words);
+  return hipGetLastError();
+}
+
+hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, const uint64_t* d_off,
+                       const uint64_t* d_len, uint64_t n, const uint32_t* d_btab, uint8_t* d_pk,
+                       uint8_t* d_sig, uint32_t max_blocks, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  uint64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > max_blocks) blocks = max_blocks;
+  hipLaunchKernelGGL(k_ed25519_sign, dim3((uint32_t)blocks), dim3(kBlock), 0, s,
+                     (const uint32_t*)d_seed, d_msg, d_off, d_len, n, d_btab, (uint32_t*)d_pk,
+                     (uint32_t*)d_sig);
+  return hipGetLastError();
+}
+
+size_t btab_bytes() { return (size_t)kBEntries * kBStride * 4; }
+size_t ws_bytes_per_slot() { return (size_t)kAEntries * kAQuads * kBlock * 16; }
+
+}  // namespace nt

@@ -1,0 +1,24 @@
+// kernels.hpp -- host-side launchers for kernels.hip (used by ntcrypto.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace nt {
+
+hipError_t launch_btab_init(uint32_t* d_tab, hipStream_t s);
+hipError_t launch_sha512_trunc32(const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
+                                 uint64_t n, uint8_t* d_out32, hipStream_t s);
+hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
+                         const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
+                         const uint32_t* d_btab, void* d_ws, uint32_t ws_slots, uint64_t* d_out_words,
+                         hipStream_t s);
+hipError_t launch_group_and(const uint64_t* d_first, const uint32_t* d_cnt, uint64_t G,
+                            const uint64_t* d_sig_words, uint64_t* d_group_words, hipStream_t s);
+hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, const uint64_t* d_off,
+                       const uint64_t* d_len, uint64_t n, const uint32_t* d_btab, uint8_t* d_pk,
+                       uint8_t* d_sig, uint32_t max_blocks, hipStream_t s);
+size_t btab_bytes();
+size_t ws_bytes_per_slot();
+
+}  // namespace nt

@@ -1,0 +1,32 @@
+// nt_common.hpp -- shared definitions for the gfx950 crypto backend.
+//
+// Device code is written as plain C++ with NT_HD (= __host__ __device__ under
+// hipcc) so that the exact same arithmetic can be exercised on the host by the
+// bound-stress test in tests/cpp/ (compiled with g++, NT_HD empty).  The
+// product library (libntcrypto.so) only ever runs it on the GPU.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define NT_HD __host__ __device__
+#define NT_D __device__
+#define NT_INLINE __attribute__((always_inline)) inline
+#else
+#define NT_HD
+#define NT_D
+#define NT_INLINE inline
+struct uint4 {
+  uint32_t x, y, z, w;
+};
+#endif
+
+namespace nt {
+
+// Kernel-facing verification modes (see include/ntcrypto.h).
+enum VerifyMode : int {
+  kStrict = 0,        // dalek verify_strict (crypto/src/lib.rs:200-204)
+  kCofactorless = 1,  // per-entry rule of dalek verify_batch, SURVEY.md A.3
+};
+
+}  // namespace nt

@@ -1,0 +1,503 @@
+// ntcrypto.cpp -- host side of the C ABI (include/ntcrypto.h).
+//
+// Owns one `Device` per GPU: a non-blocking HIP stream, the [j]B table, the
+// per-lane [k]A table workspace and grow-only device/pinned staging buffers.
+// Host entry points shard items over devices by contiguous index ranges (one
+// host thread per device), stage through pinned memory, launch, and gather the
+// bitmaps / digests.  There is deliberately no CPU compute path: if HIP or the
+// gfx950 code object is unavailable the call fails with a negative code.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/ntcrypto.h"
+#include "kernels.hpp"
+
+namespace {
+
+#define NT_TRY(expr)                       \
+  do {                                     \
+    hipError_t _e = (expr);                \
+    if (_e != hipSuccess) return NT_EHIP;  \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return NT_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 1 << 16);
+    want = (want + 4095) & ~(size_t)4095;
+    if (hipMalloc(&p, want) != hipSuccess) return NT_ENOMEM;
+    cap = want;
+    return NT_OK;
+  }
+  template <class T>
+  T* as() const { return (T*)p; }
+};
+
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return NT_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 1 << 16);
+    want = (want + 4095) & ~(size_t)4095;
+    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return NT_ENOMEM;
+    cap = want;
+    return NT_OK;
+  }
+  template <class T>
+  T* as() const { return (T*)p; }
+};
+
+enum { B_DATA, B_OFF, B_LEN, B_PK, B_SIG, B_OUT, B_OUT2, B_FIRST, B_CNT, B_NBUF };
+
+struct Device {
+  int ordinal = -1;
+  hipStream_t stream = nullptr;
+  uint32_t* d_btab = nullptr;
+  void* d_ws = nullptr;
+  uint32_t ws_slots = 0;
+  uint32_t sign_blocks = 0;
+  hipEvent_t ws_done = nullptr;  // orders every kernel that uses d_ws, whatever its stream
+  std::mutex mu;
+  DevBuf d[B_NBUF];
+  HostBuf h[B_NBUF];
+
+  ~Device() {
+    if (ordinal < 0) return;
+    (void)hipSetDevice(ordinal);
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto& b : d)
+      if (b.p) (void)hipFree(b.p);
+    for (auto& b : h)
+      if (b.p) (void)hipHostFree(b.p);
+    if (d_btab) (void)hipFree(d_btab);
+    if (d_ws) (void)hipFree(d_ws);
+    if (ws_done) (void)hipEventDestroy(ws_done);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  int init(int ord) {
+    ordinal = ord;
+    NT_TRY(hipSetDevice(ord));
+    hipDeviceProp_t prop;
+    NT_TRY(hipGetDeviceProperties(&prop, ord));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NT_ENODEV;
+    NT_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    NT_TRY(hipEventCreateWithFlags(&ws_done, hipEventDisableTiming));
+    NT_TRY(hipMalloc(&d_btab, nt::btab_bytes()));
+    NT_TRY(nt::launch_btab_init(d_btab, stream));
+    // one workspace slot per resident workgroup; default 4 per CU
+    uint32_t slots = (uint32_t)prop.multiProcessorCount * 4;
+    if (const char* e = std::getenv("NT_WS_SLOTS")) slots = (uint32_t)std::max(1, std::atoi(e));
+    ws_slots = slots;
+    sign_blocks = (uint32_t)prop.multiProcessorCount * 8;
+    if (hipMalloc(&d_ws, nt::ws_bytes_per_slot() * ws_slots) != hipSuccess) return NT_ENOMEM;
+    NT_TRY(hipEventRecord(ws_done, stream));
+    NT_TRY(hipStreamSynchronize(stream));
+    return NT_OK;
+  }
+
+  // verify launch that shares the workspace: wait for the previous user, then mark
+  hipError_t verify(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                    const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out,
+                    hipStream_t s) {
+    hipError_t e = hipStreamWaitEvent(s, ws_done, 0);
+    if (e != hipSuccess) return e;
+    e = nt::launch_verify(mode, pk, sig, msg, off, len, n, d_btab, d_ws, ws_slots, out, s);
+    if (e != hipSuccess) return e;
+    return hipEventRecord(ws_done, s);
+  }
+};
+
+}  // namespace
+
+struct nt_ctx {
+  std::vector<std::unique_ptr<Device>> devs;
+};
+
+extern "C" {
+
+const char* nt_strerror(int code) {
+  switch (code) {
+    case NT_OK: return "ok";
+    case NT_EINVAL: return "invalid argument";
+    case NT_EHIP: return "HIP runtime error";
+    case NT_ENOMEM: return "out of device or pinned memory";
+    case NT_ENODEV: return "no usable gfx950 device (this library has no CPU path)";
+    default: return "unknown error";
+  }
+}
+
+const char* nt_version(void) { return "ntcrypto 0.1 gfx950"; }
+
+static int init_common(nt_ctx** out, const std::vector<int>& ords) {
+  if (!out) return NT_EINVAL;
+  *out = nullptr;
+  auto ctx = std::make_unique<nt_ctx>();
+  for (int o : ords) {
+    auto d = std::make_unique<Device>();
+    const int rc = d->init(o);
+    if (rc != NT_OK) return rc;
+    ctx->devs.push_back(std::move(d));
+  }
+  if (ctx->devs.empty()) return NT_ENODEV;
+  *out = ctx.release();
+  return NT_OK;
+}
+
+int nt_init(nt_ctx** out, int num_gpus) {
+  if (num_gpus < 0) return NT_ENODEV;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return NT_ENODEV;
+  if (num_gpus == 0 || num_gpus > count) num_gpus = count;
+  std::vector<int> ords;
+  for (int i = 0; i < num_gpus; ++i) ords.push_back(i);
+  return init_common(out, ords);
+}
+
+int nt_init_device(nt_ctx** out, int device_ordinal) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return NT_ENODEV;
+  if (device_ordinal < 0 || device_ordinal >= count) return NT_EINVAL;
+  return init_common(out, {device_ordinal});
+}
+
+void nt_free(nt_ctx* ctx) { delete ctx; }
+
+int nt_num_devices(const nt_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+}  // extern "C"
+
+namespace {
+
+// Split [0, n) into one contiguous range per device, boundaries multiple of `align`.
+std::vector<std::pair<uint64_t, uint64_t>> shard(uint64_t n, size_t ndev, uint64_t align) {
+  std::vector<std::pair<uint64_t, uint64_t>> r;
+  uint64_t per = (n + ndev - 1) / ndev;
+  per = (per + align - 1) / align * align;
+  uint64_t lo = 0;
+  for (size_t d = 0; d < ndev; ++d) {
+    const uint64_t hi = std::min(n, lo + per);
+    r.emplace_back(lo, hi);
+    lo = hi;
+  }
+  return r;
+}
+
+template <class F>
+int run_sharded(nt_ctx* ctx, uint64_t n, uint64_t align, F&& fn) {
+  const size_t nd = ctx->devs.size();
+  auto parts = shard(n, nd, align);
+  if (nd == 1) {
+    Device& dv = *ctx->devs[0];
+    std::lock_guard<std::mutex> lk(dv.mu);
+    if (hipSetDevice(dv.ordinal) != hipSuccess) return NT_EHIP;
+    return fn(dv, parts[0].first, parts[0].second);
+  }
+  std::vector<int> rcs(nd, NT_OK);
+  std::vector<std::thread> th;
+  for (size_t d = 0; d < nd; ++d) {
+    if (parts[d].first >= parts[d].second) continue;
+    th.emplace_back([&, d] {
+      Device& dv = *ctx->devs[d];
+      std::lock_guard<std::mutex> lk(dv.mu);
+      if (hipSetDevice(dv.ordinal) != hipSuccess) {
+        rcs[d] = NT_EHIP;
+        return;
+      }
+      rcs[d] = fn(dv, parts[d].first, parts[d].second);
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int rc : rcs)
+    if (rc != NT_OK) return rc;
+  return NT_OK;
+}
+
+#define NT_CHK(expr)              \
+  do {                            \
+    int _rc = (expr);             \
+    if (_rc != NT_OK) return _rc; \
+  } while (0)
+
+// Stage the message span used by items [lo, hi) (rebased offsets, 16-B phase kept).
+int stage_messages(Device& dv, const uint8_t* data, const uint64_t* off, const uint64_t* len,
+                   uint64_t lo, uint64_t hi, uint64_t* base_out) {
+  uint64_t mn = UINT64_MAX, mx = 0;
+  for (uint64_t i = lo; i < hi; ++i) {
+    if (len[i] == 0) continue;
+    mn = std::min(mn, off[i]);
+    mx = std::max(mx, off[i] + len[i]);
+  }
+  if (mn == UINT64_MAX) mn = mx = 0;
+  const uint64_t base = mn & ~(uint64_t)15;
+  const uint64_t span = mx - base;
+  const uint64_t m = hi - lo;
+  NT_CHK(dv.d[B_DATA].ensure(span + 64));
+  NT_CHK(dv.d[B_OFF].ensure(m * 8));
+  NT_CHK(dv.d[B_LEN].ensure(m * 8));
+  NT_CHK(dv.h[B_OFF].ensure(m * 8));
+  NT_CHK(dv.h[B_LEN].ensure(m * 8));
+  uint64_t* ho = dv.h[B_OFF].as<uint64_t>();
+  uint64_t* hl = dv.h[B_LEN].as<uint64_t>();
+  for (uint64_t i = lo; i < hi; ++i) {
+    ho[i - lo] = len[i] ? off[i] - base : 0;
+    hl[i - lo] = len[i];
+  }
+  if (span) NT_TRY(hipMemcpyAsync(dv.d[B_DATA].p, data + base, span, hipMemcpyHostToDevice, dv.stream));
+  NT_TRY(hipMemcpyAsync(dv.d[B_OFF].p, ho, m * 8, hipMemcpyHostToDevice, dv.stream));
+  NT_TRY(hipMemcpyAsync(dv.d[B_LEN].p, hl, m * 8, hipMemcpyHostToDevice, dv.stream));
+  *base_out = base;
+  return NT_OK;
+}
+
+void words_to_bitmap(uint8_t* out, const uint64_t* words, uint64_t nbits) {
+  const uint64_t nbytes = (nbits + 7) / 8;
+  std::memcpy(out, words, nbytes);  // little-endian words == LSB-first bytes
+  if (nbits & 7) out[nbytes - 1] &= (uint8_t)((1u << (nbits & 7)) - 1);
+}
+
+Device* dev_of(nt_ctx* ctx, int dev) {
+  if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return nullptr;
+  return ctx->devs[dev].get();
+}
+
+}  // namespace
+
+extern "C" {
+
+int nt_sha512_trunc32(nt_ctx* ctx, const uint8_t* data, const uint64_t* off, const uint64_t* len,
+                      uint64_t n, uint8_t* out32) {
+  if (!ctx || (n && (!off || !len || !out32))) return NT_EINVAL;
+  if (n == 0) return NT_OK;
+  return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
+    uint64_t base;
+    NT_CHK(stage_messages(dv, data, off, len, lo, hi, &base));
+    const uint64_t m = hi - lo;
+    NT_CHK(dv.d[B_OUT].ensure(m * 32));
+    NT_TRY(nt::launch_sha512_trunc32(dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>(),
+                                     dv.d[B_LEN].as<uint64_t>(), m, dv.d[B_OUT].as<uint8_t>(),
+                                     dv.stream));
+    NT_TRY(hipMemcpyAsync(out32 + 32 * lo, dv.d[B_OUT].p, m * 32, hipMemcpyDeviceToHost, dv.stream));
+    NT_TRY(hipStreamSynchronize(dv.stream));
+    return NT_OK;
+  });
+}
+
+int nt_ed25519_verify_strict(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* sig64,
+                             const uint8_t* msg, const uint64_t* off, const uint64_t* len,
+                             uint64_t n, uint8_t* out_bitmap) {
+  if (!ctx || (n && (!pk32 || !sig64 || !off || !len || !out_bitmap))) return NT_EINVAL;
+  if (n == 0) return NT_OK;
+  return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
+    uint64_t base;
+    NT_CHK(stage_messages(dv, msg, off, len, lo, hi, &base));
+    const uint64_t m = hi - lo, words = (m + 63) / 64;
+    NT_CHK(dv.d[B_PK].ensure(m * 32));
+    NT_CHK(dv.d[B_SIG].ensure(m * 64));
+    NT_CHK(dv.d[B_OUT].ensure(words * 8));
+    NT_CHK(dv.h[B_OUT].ensure(words * 8));
+    NT_TRY(hipMemcpyAsync(dv.d[B_PK].p, pk32 + 32 * lo, m * 32, hipMemcpyHostToDevice, dv.stream));
+    NT_TRY(hipMemcpyAsync(dv.d[B_SIG].p, sig64 + 64 * lo, m * 64, hipMemcpyHostToDevice, dv.stream));
+    NT_TRY(dv.verify(NT_MODE_STRICT, dv.d[B_PK].as<uint8_t>(), dv.d[B_SIG].as<uint8_t>(),
+                     dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>(),
+                     dv.d[B_LEN].as<uint64_t>(), m, dv.d[B_OUT].as<uint64_t>(), dv.stream));
+    NT_TRY(hipMemcpyAsync(dv.h[B_OUT].p, dv.d[B_OUT].p, words * 8, hipMemcpyDeviceToHost, dv.stream));
+    NT_TRY(hipStreamSynchronize(dv.stream));
+    words_to_bitmap(out_bitmap + lo / 8, dv.h[B_OUT].as<uint64_t>(), m);
+    return NT_OK;
+  });
+}
+
+int nt_ed25519_verify_batch_groups(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* sig64,
+                                   const uint64_t* first, const uint32_t* cnt,
+                                   const uint8_t* msg32, uint64_t G, uint8_t* out_group_bitmap,
+                                   uint8_t* out_sig_bitmap) {
+  if (!ctx || (G && (!first || !cnt || !msg32 || !out_group_bitmap))) return NT_EINVAL;
+  if (G == 0) return NT_OK;
+  uint64_t nsig_total = 0;
+  for (uint64_t g = 0; g < G; ++g) nsig_total = std::max(nsig_total, first[g] + cnt[g]);
+  if (nsig_total && (!pk32 || !sig64)) return NT_EINVAL;
+  if (out_sig_bitmap) std::memset(out_sig_bitmap, 0, (nsig_total + 7) / 8);
+  std::mutex sig_mu;
+  return run_sharded(ctx, G, 64, [&](Device& dv, uint64_t glo, uint64_t ghi) -> int {
+    const uint64_t gm = ghi - glo;
+    uint64_t m = 0;
+    for (uint64_t g = glo; g < ghi; ++g) m += cnt[g];
+    const uint64_t sw = (m + 63) / 64, gw = (gm + 63) / 64;
+    const uint64_t mm = std::max<uint64_t>(m, 1);
+    NT_CHK(dv.h[B_PK].ensure(mm * 32));
+    NT_CHK(dv.h[B_SIG].ensure(mm * 64));
+    NT_CHK(dv.h[B_OFF].ensure(mm * 8));
+    NT_CHK(dv.h[B_LEN].ensure(mm * 8));
+    NT_CHK(dv.h[B_FIRST].ensure(gm * 8));
+    NT_CHK(dv.h[B_CNT].ensure(gm * 4));
+    NT_CHK(dv.h[B_OUT].ensure(sw * 8 + 8));
+    NT_CHK(dv.h[B_OUT2].ensure(gw * 8));
+    uint8_t* hpk = dv.h[B_PK].as<uint8_t>();
+    uint8_t* hsig = dv.h[B_SIG].as<uint8_t>();
+    uint64_t* hoff = dv.h[B_OFF].as<uint64_t>();
+    uint64_t* hlen = dv.h[B_LEN].as<uint64_t>();
+    uint64_t* hfirst = dv.h[B_FIRST].as<uint64_t>();
+    uint32_t* hcnt = dv.h[B_CNT].as<uint32_t>();
+    uint64_t e = 0;
+    for (uint64_t g = glo; g < ghi; ++g) {
+      hfirst[g - glo] = e;
+      hcnt[g - glo] = cnt[g];
+      if (cnt[g]) {
+        std::memcpy(hpk + 32 * e, pk32 + 32 * first[g], 32ull * cnt[g]);
+        std::memcpy(hsig + 64 * e, sig64 + 64 * first[g], 64ull * cnt[g]);
+      }
+      for (uint32_t t = 0; t < cnt[g]; ++t) {
+        hoff[e + t] = 32 * (g - glo);
+        hlen[e + t] = 32;
+      }
+      e += cnt[g];
+    }
+    NT_CHK(dv.d[B_PK].ensure(mm * 32));
+    NT_CHK(dv.d[B_SIG].ensure(mm * 64));
+    NT_CHK(dv.d[B_OFF].ensure(mm * 8));
+    NT_CHK(dv.d[B_LEN].ensure(mm * 8));
+    NT_CHK(dv.d[B_DATA].ensure(gm * 32 + 64));
+    NT_CHK(dv.d[B_FIRST].ensure(gm * 8));
+    NT_CHK(dv.d[B_CNT].ensure(gm * 4));
+    NT_CHK(dv.d[B_OUT].ensure(sw * 8 + 8));
+    NT_CHK(dv.d[B_OUT2].ensure(gw * 8));
+    hipStream_t s = dv.stream;
+    if (m) {
+      NT_TRY(hipMemcpyAsync(dv.d[B_PK].p, hpk, m * 32, hipMemcpyHostToDevice, s));
+      NT_TRY(hipMemcpyAsync(dv.d[B_SIG].p, hsig, m * 64, hipMemcpyHostToDevice, s));
+      NT_TRY(hipMemcpyAsync(dv.d[B_OFF].p, hoff, m * 8, hipMemcpyHostToDevice, s));
+      NT_TRY(hipMemcpyAsync(dv.d[B_LEN].p, hlen, m * 8, hipMemcpyHostToDevice, s));
+    }
+    NT_TRY(hipMemcpyAsync(dv.d[B_DATA].p, msg32 + 32 * glo, gm * 32, hipMemcpyHostToDevice, s));
+    NT_TRY(hipMemcpyAsync(dv.d[B_FIRST].p, hfirst, gm * 8, hipMemcpyHostToDevice, s));
+    NT_TRY(hipMemcpyAsync(dv.d[B_CNT].p, hcnt, gm * 4, hipMemcpyHostToDevice, s));
+    NT_TRY(hipMemsetAsync(dv.d[B_OUT].p, 0, sw * 8 + 8, s));
+    NT_TRY(dv.verify(NT_MODE_COFACTORLESS, dv.d[B_PK].as<uint8_t>(), dv.d[B_SIG].as<uint8_t>(),
+                     dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>(),
+                     dv.d[B_LEN].as<uint64_t>(), m, dv.d[B_OUT].as<uint64_t>(), s));
+    NT_TRY(nt::launch_group_and(dv.d[B_FIRST].as<uint64_t>(), dv.d[B_CNT].as<uint32_t>(), gm,
+                                dv.d[B_OUT].as<uint64_t>(), dv.d[B_OUT2].as<uint64_t>(), s));
+    NT_TRY(hipMemcpyAsync(dv.h[B_OUT2].p, dv.d[B_OUT2].p, gw * 8, hipMemcpyDeviceToHost, s));
+    if (out_sig_bitmap && m)
+      NT_TRY(hipMemcpyAsync(dv.h[B_OUT].p, dv.d[B_OUT].p, sw * 8, hipMemcpyDeviceToHost, s));
+    NT_TRY(hipStreamSynchronize(s));
+    words_to_bitmap(out_group_bitmap + glo / 8, dv.h[B_OUT2].as<uint64_t>(), gm);
+    if (out_sig_bitmap && m) {
+      const uint64_t* bits = dv.h[B_OUT].as<uint64_t>();
+      std::lock_guard<std::mutex> lk(sig_mu);
+      uint64_t e2 = 0;
+      for (uint64_t g = glo; g < ghi; ++g) {
+        for (uint32_t t = 0; t < cnt[g]; ++t, ++e2) {
+          if ((bits[e2 >> 6] >> (e2 & 63)) & 1) {
+            const uint64_t o = first[g] + t;
+            out_sig_bitmap[o >> 3] |= (uint8_t)(1u << (o & 7));
+          }
+        }
+      }
+    }
+    return NT_OK;
+  });
+}
+
+int nt_ed25519_sign_batch(nt_ctx* ctx, const uint8_t* seed32, const uint8_t* msg,
+                          const uint64_t* off, const uint64_t* len, uint64_t n, uint8_t* pk32,
+                          uint8_t* sig64) {
+  if (!ctx || (n && (!seed32 || !pk32))) return NT_EINVAL;
+  if (sig64 && n && (!off || !len)) return NT_EINVAL;
+  if (n == 0) return NT_OK;
+  return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
+    const uint64_t m = hi - lo;
+    const uint8_t* d_msg = nullptr;
+    const uint64_t *d_off = nullptr, *d_len = nullptr;
+    if (sig64) {
+      uint64_t base;
+      NT_CHK(stage_messages(dv, msg, off, len, lo, hi, &base));
+      d_msg = dv.d[B_DATA].as<uint8_t>();
+      d_off = dv.d[B_OFF].as<uint64_t>();
+      d_len = dv.d[B_LEN].as<uint64_t>();
+    }
+    NT_CHK(dv.d[B_PK].ensure(m * 32));
+    NT_CHK(dv.d[B_SIG].ensure(m * 64));
+    NT_CHK(dv.d[B_OUT].ensure(m * 32));
+    NT_TRY(hipMemcpyAsync(dv.d[B_OUT].p, seed32 + 32 * lo, m * 32, hipMemcpyHostToDevice, dv.stream));
+    NT_TRY(nt::launch_sign(dv.d[B_OUT].as<uint8_t>(), d_msg, d_off, d_len, m, dv.d_btab,
+                           dv.d[B_PK].as<uint8_t>(), sig64 ? dv.d[B_SIG].as<uint8_t>() : nullptr,
+                           dv.sign_blocks, dv.stream));
+    NT_TRY(hipMemcpyAsync(pk32 + 32 * lo, dv.d[B_PK].p, m * 32, hipMemcpyDeviceToHost, dv.stream));
+    if (sig64)
+      NT_TRY(hipMemcpyAsync(sig64 + 64 * lo, dv.d[B_SIG].p, m * 64, hipMemcpyDeviceToHost, dv.stream));
+    NT_TRY(hipStreamSynchronize(dv.stream));
+    return NT_OK;
+  });
+}
+
+int nt_ed25519_keypair_batch(nt_ctx* ctx, const uint8_t* seed32, uint64_t n, uint8_t* pk32) {
+  return nt_ed25519_sign_batch(ctx, seed32, nullptr, nullptr, nullptr, n, pk32, nullptr);
+}
+
+// ---- device-resident entry points ---------------------------------------
+int nt_dev_sha512_trunc32(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_data,
+                          const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
+                          uint8_t* d_out32) {
+  Device* dv = dev_of(ctx, dev);
+  if (!dv) return NT_EINVAL;
+  NT_TRY(hipSetDevice(dv->ordinal));
+  hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
+  NT_TRY(nt::launch_sha512_trunc32(d_data, d_off, d_len, n, d_out32, s));
+  return NT_OK;
+}
+
+int nt_dev_ed25519_verify(nt_ctx* ctx, int dev, void* stream, int mode, const uint8_t* d_pk32,
+                          const uint8_t* d_sig64, const uint8_t* d_msg, const uint64_t* d_off,
+                          const uint64_t* d_len, uint64_t n, uint64_t* d_out_words) {
+  Device* dv = dev_of(ctx, dev);
+  if (!dv || (mode != NT_MODE_STRICT && mode != NT_MODE_COFACTORLESS)) return NT_EINVAL;
+  NT_TRY(hipSetDevice(dv->ordinal));
+  hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
+  // the [k]A workspace is per device: serialize launches that use it
+  std::lock_guard<std::mutex> lk(dv->mu);
+  NT_TRY(dv->verify(mode, d_pk32, d_sig64, d_msg, d_off, d_len, n, d_out_words, s));
+  return NT_OK;
+}
+
+int nt_dev_group_and(nt_ctx* ctx, int dev, void* stream, const uint64_t* d_first,
+                     const uint32_t* d_cnt, uint64_t G, const uint64_t* d_sig_words,
+                     uint64_t* d_group_words) {
+  Device* dv = dev_of(ctx, dev);
+  if (!dv) return NT_EINVAL;
+  NT_TRY(hipSetDevice(dv->ordinal));
+  hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
+  NT_TRY(nt::launch_group_and(d_first, d_cnt, G, d_sig_words, d_group_words, s));
+  return NT_OK;
+}
+
+int nt_dev_ed25519_sign(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_seed32,
+                        const uint8_t* d_msg, const uint64_t* d_off, const uint64_t* d_len,
+                        uint64_t n, uint8_t* d_pk32, uint8_t* d_sig64) {
+  Device* dv = dev_of(ctx, dev);
+  if (!dv) return NT_EINVAL;
+  NT_TRY(hipSetDevice(dv->ordinal));
+  hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
+  NT_TRY(nt::launch_sign(d_seed32, d_msg, d_off, d_len, n, dv->d_btab, d_pk32, d_sig64,
+                         dv->sign_blocks, s));
+  return NT_OK;
+}
+
+}  // extern "C"

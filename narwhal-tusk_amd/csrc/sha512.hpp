@@ -1,0 +1,197 @@
+// sha512.hpp -- FIPS 180-4 SHA-512 for one lane per message on gfx950.
+//
+// 64-bit rotates lower to v_alignbit_b32 pairs, 64-bit adds to v_lshl_add_u64 /
+// v_add_co+v_addc, Ch/Maj to v_bfi_b32; big-endian word loads are byte-swapped
+// with v_perm_b32.  The 16-entry circular message schedule keeps the state in
+// 8 + 16 64-bit registers (48 VGPRs).
+//
+// Streams: the hashed byte string is  prefix (PW 32-bit words held in
+// registers, 4*PW < 128)  ||  msg[0..len)  (global memory, any alignment).
+//   PW = 0  : batch digests        worker/src/processor.rs:38
+//   PW = 16 : k = H(R || A || M)    dalek verify_strict / verify_batch
+//   PW = 8  : r = H(prefix || M)    RFC 8032 signing (crypto/src/lib.rs:185-191)
+#pragma once
+#include "nt_common.hpp"
+
+namespace nt {
+
+#if defined(__HIP_DEVICE_COMPILE__)
+__constant__ static const uint64_t kSha512K[80] = {
+#else
+static const uint64_t kSha512K[80] = {
+#endif
+    0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+    0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+    0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+    0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+    0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+    0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+    0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+    0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+    0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+    0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+    0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+    0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+    0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+    0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+    0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+    0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+    0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+    0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+    0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+    0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+
+NT_HD NT_INLINE uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+NT_HD NT_INLINE uint32_t bswap32(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_bswap32(x);
+#else
+  return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+#endif
+}
+
+NT_HD NT_INLINE void sha512_init(uint64_t st[8]) {
+  st[0] = 0x6a09e667f3bcc908ULL; st[1] = 0xbb67ae8584caa73bULL;
+  st[2] = 0x3c6ef372fe94f82bULL; st[3] = 0xa54ff53a5f1d36f1ULL;
+  st[4] = 0x510e527fade682d1ULL; st[5] = 0x9b05688c2b3e6c1fULL;
+  st[6] = 0x1f83d9abfb41bd6bULL; st[7] = 0x5be0cd19137e2179ULL;
+}
+
+#define NT_SHA_ROUND(a, b, c, d, e, f, g, h, kw)                                   \
+  {                                                                                \
+    const uint64_t t1 = h + (rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41)) +      \
+                        ((e & f) ^ (~e & g)) + (kw);                               \
+    const uint64_t t2 = (rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39)) +          \
+                        ((a & b) ^ (a & c) ^ (b & c));                             \
+    d += t1;                                                                       \
+    h = t1 + t2;                                                                   \
+  }
+
+// One compression. blk[i] = LE 32-bit words of the 128-byte block as stored in memory.
+NT_HD NT_INLINE void sha512_compress_words(uint64_t st[8], const uint32_t blk[32]) {
+  uint64_t W[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t)
+    W[t] = ((uint64_t)bswap32(blk[2 * t]) << 32) | bswap32(blk[2 * t + 1]);
+  uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+  for (int r = 0; r < 80; r += 8) {
+    if (r >= 16) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int i = (r + t) & 15;
+        const uint64_t w15 = W[(i + 1) & 15], w2 = W[(i + 14) & 15];
+        const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
+        const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
+        W[i] += s0 + W[(i + 9) & 15] + s1;
+      }
+    }
+    NT_SHA_ROUND(a, b, c, d, e, f, g, h, kSha512K[r + 0] + W[(r + 0) & 15]);
+    NT_SHA_ROUND(h, a, b, c, d, e, f, g, kSha512K[r + 1] + W[(r + 1) & 15]);
+    NT_SHA_ROUND(g, h, a, b, c, d, e, f, kSha512K[r + 2] + W[(r + 2) & 15]);
+    NT_SHA_ROUND(f, g, h, a, b, c, d, e, kSha512K[r + 3] + W[(r + 3) & 15]);
+    NT_SHA_ROUND(e, f, g, h, a, b, c, d, kSha512K[r + 4] + W[(r + 4) & 15]);
+    NT_SHA_ROUND(d, e, f, g, h, a, b, c, kSha512K[r + 5] + W[(r + 5) & 15]);
+    NT_SHA_ROUND(c, d, e, f, g, h, a, b, kSha512K[r + 6] + W[(r + 6) & 15]);
+    NT_SHA_ROUND(b, c, d, e, f, g, h, a, kSha512K[r + 7] + W[(r + 7) & 15]);
+  }
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// Load NW little-endian words starting at byte address p (any alignment) from
+// an interval that contains all of [p, p + 4 NW).  Aligned dword loads +
+// v_alignbyte_b32; the extra word is only fetched when p is misaligned and it
+// then shares a 4-byte granule with the last wanted byte.
+template <int NW>
+NT_HD NT_INLINE void load_words(uint32_t* w, const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t sh = (uint32_t)(a & 3u);
+  const uint32_t* pw = (const uint32_t*)(a & ~(uintptr_t)3);
+  if (sh == 0) {
+    if ((a & 15u) == 0 && (NW % 4) == 0) {
+#pragma unroll
+      for (int i = 0; i < NW / 4; ++i) {
+        const uint4 q = ((const uint4*)pw)[i];
+        w[4 * i] = q.x; w[4 * i + 1] = q.y; w[4 * i + 2] = q.z; w[4 * i + 3] = q.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NW; ++i) w[i] = pw[i];
+    }
+  } else {
+    uint32_t prev = pw[0];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const uint32_t nxt = pw[i + 1];
+#if defined(__HIP_DEVICE_COMPILE__)
+      w[i] = __builtin_amdgcn_alignbyte(nxt, prev, sh);
+#else
+      w[i] = (uint32_t)((((uint64_t)nxt << 32) | prev) >> (8 * sh));
+#endif
+      prev = nxt;
+    }
+  }
+}
+
+// Hash  prefix[0..PW) || msg[0..len)  and return the 8 state words.
+template <int PW>
+NT_HD NT_INLINE void sha512_prefixed(uint64_t st[8], const uint32_t* prefix, const uint8_t* msg,
+                                     uint64_t len) {
+  sha512_init(st);
+  const uint64_t total = (uint64_t)(4 * PW) + len;
+  const uint64_t nblocks = (total + 17 + 127) / 128;
+  const uint64_t nfull = total / 128;  // blocks made only of prefix/message bytes
+  uint32_t blk[32];
+  for (uint64_t b = 0; b < nblocks; ++b) {
+    if (b < nfull) {
+      if (b == 0) {
+#pragma unroll
+        for (int i = 0; i < PW; ++i) blk[i] = prefix[i];
+        load_words<32 - PW>(blk + PW, msg);
+      } else {
+        load_words<32>(blk, msg + (128 * b - 4 * PW));
+      }
+    } else {
+      // tail block(s): bytes beyond the message, 0x80, zeros, 128-bit length
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        uint32_t wv = 0;
+        if (i < PW && b == 0) {
+          wv = prefix[i < PW ? i : 0];  // prefix words are whole words of block 0
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint64_t pos = 128 * b + 4 * i + j;  // position in the stream
+            uint32_t byte;
+            if (pos < total) {
+              byte = msg[pos - 4 * PW];
+            } else {
+              byte = (pos == total) ? 0x80u : 0u;
+            }
+            wv |= byte << (8 * j);
+          }
+        }
+        blk[i] = wv;
+      }
+      if (b == nblocks - 1) {
+        const uint64_t bits = total << 3;
+        blk[28] = 0;
+        blk[29] = bswap32((uint32_t)(total >> 61));
+        blk[30] = bswap32((uint32_t)(bits >> 32));
+        blk[31] = bswap32((uint32_t)bits);
+      }
+    }
+    sha512_compress_words(st, blk);
+  }
+}
+
+// First 32 bytes / all 64 bytes of the digest as little-endian memory words.
+NT_HD NT_INLINE void sha512_out_words(uint32_t* out, const uint64_t st[8], int nwords) {
+  for (int i = 0; i < nwords / 2; ++i) {
+    out[2 * i] = bswap32((uint32_t)(st[i] >> 32));
+    out[2 * i + 1] = bswap32((uint32_t)st[i]);
+  }
+}
+
+}  // namespace nt

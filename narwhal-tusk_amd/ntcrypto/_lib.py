@@ -1,0 +1,206 @@
+"""ctypes binding of libntcrypto.so (include/ntcrypto.h).
+
+The product path: every call goes to the gfx950 HIP kernels through the C ABI.
+There is no CPU fallback -- if the library or a gfx950 device is missing the
+calls raise NtError.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("NTCRYPTO_LIB", os.path.join(PKG_ROOT, "lib", "libntcrypto.so"))
+
+NT_MODE_STRICT = 0
+NT_MODE_COFACTORLESS = 1
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_vp = ctypes.c_void_p
+_u64 = ctypes.c_uint64
+
+EXPORTED = [
+    "nt_init", "nt_init_device", "nt_free", "nt_num_devices", "nt_strerror", "nt_version",
+    "nt_sha512_trunc32", "nt_ed25519_verify_strict", "nt_ed25519_verify_batch_groups",
+    "nt_ed25519_sign_batch", "nt_ed25519_keypair_batch", "nt_dev_sha512_trunc32",
+    "nt_dev_ed25519_verify", "nt_dev_group_and", "nt_dev_ed25519_sign",
+]
+
+
+class NtError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load_library(path=None):
+    """Load libntcrypto.so and declare prototypes (no GPU needed)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise NtError("libntcrypto.so not built (%s); run `make -C narwhal-tusk_amd`" % p)
+    lib = ctypes.CDLL(p)
+    lib.nt_init.argtypes = [ctypes.POINTER(_vp), ctypes.c_int]
+    lib.nt_init_device.argtypes = [ctypes.POINTER(_vp), ctypes.c_int]
+    lib.nt_free.argtypes = [_vp]
+    lib.nt_free.restype = None
+    lib.nt_num_devices.argtypes = [_vp]
+    lib.nt_strerror.restype = ctypes.c_char_p
+    lib.nt_version.restype = ctypes.c_char_p
+    lib.nt_sha512_trunc32.argtypes = [_vp, _u8p, _u64p, _u64p, _u64, _u8p]
+    lib.nt_ed25519_verify_strict.argtypes = [_vp, _u8p, _u8p, _u8p, _u64p, _u64p, _u64, _u8p]
+    lib.nt_ed25519_verify_batch_groups.argtypes = [_vp, _u8p, _u8p, _u64p, _u32p, _u8p, _u64, _u8p, _u8p]
+    lib.nt_ed25519_sign_batch.argtypes = [_vp, _u8p, _u8p, _u64p, _u64p, _u64, _u8p, _u8p]
+    lib.nt_ed25519_keypair_batch.argtypes = [_vp, _u8p, _u64, _u8p]
+    lib.nt_dev_sha512_trunc32.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, _u64, _vp]
+    lib.nt_dev_ed25519_verify.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_int, _vp, _vp, _vp, _vp, _vp,
+                                          _u64, _vp]
+    lib.nt_dev_group_and.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _u64, _vp, _vp]
+    lib.nt_dev_ed25519_sign.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp]
+    _lib = lib
+    return lib
+
+
+def _p(a, t=_u8p):
+    return a.ctypes.data_as(t)
+
+
+def _u8(a, shape_tail=None):
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    return a
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise NtError("%s failed: %s (%d)" % (what, load_library().nt_strerror(rc).decode(), rc))
+
+
+def _unpack(bm, n):
+    return np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+
+
+class Backend:
+    """A context over one or more gfx950 devices (nt_init / nt_init_device)."""
+
+    def __init__(self, num_gpus=0, device=None):
+        self.lib = load_library()
+        ctx = _vp()
+        if device is not None:
+            rc = self.lib.nt_init_device(ctypes.byref(ctx), int(device))
+        else:
+            rc = self.lib.nt_init(ctypes.byref(ctx), int(num_gpus))
+        _check(rc, "nt_init")
+        self.ctx = ctx
+
+    def close(self):
+        if self.ctx:
+            self.lib.nt_free(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def num_devices(self):
+        return self.lib.nt_num_devices(self.ctx)
+
+    # ---- SHA-512 ----
+    def sha512_trunc32(self, data, off, ln):
+        data = _u8(data) if len(data) else np.zeros(1, np.uint8)
+        off = np.ascontiguousarray(off, np.uint64)
+        ln = np.ascontiguousarray(ln, np.uint64)
+        n = len(off)
+        out = np.zeros((max(n, 1), 32), np.uint8)
+        _check(self.lib.nt_sha512_trunc32(self.ctx, _p(data), _p(off, _u64p), _p(ln, _u64p), n, _p(out)),
+               "nt_sha512_trunc32")
+        return out[:n]
+
+    def digest_many(self, messages):
+        ln = np.array([len(m) for m in messages], np.uint64)
+        off = np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.uint64) if len(messages) else np.zeros(0, np.uint64)
+        data = np.frombuffer(b"".join(messages), np.uint8) if messages else np.zeros(0, np.uint8)
+        return self.sha512_trunc32(data, off, ln)
+
+    # ---- Ed25519 ----
+    def verify_strict(self, pk, sig, msg, off, ln):
+        pk = _u8(pk).reshape(-1, 32)
+        sig = _u8(sig).reshape(-1, 64)
+        n = len(pk)
+        msg = _u8(msg) if len(msg) else np.zeros(1, np.uint8)
+        off = np.ascontiguousarray(off, np.uint64)
+        ln = np.ascontiguousarray(ln, np.uint64)
+        bm = np.zeros((n + 7) // 8 + 1, np.uint8)
+        _check(self.lib.nt_ed25519_verify_strict(self.ctx, _p(pk), _p(sig), _p(msg), _p(off, _u64p),
+                                                  _p(ln, _u64p), n, _p(bm)), "nt_ed25519_verify_strict")
+        return _unpack(bm, n)
+
+    def verify_batch_groups(self, pk, sig, first, cnt, msg32, with_sig_bits=False):
+        pk = _u8(pk).reshape(-1, 32)
+        sig = _u8(sig).reshape(-1, 64)
+        if len(pk) == 0:
+            pk = np.zeros((1, 32), np.uint8)
+            sig = np.zeros((1, 64), np.uint8)
+        first = np.ascontiguousarray(first, np.uint64)
+        cnt = np.ascontiguousarray(cnt, np.uint32)
+        msg32 = _u8(msg32).reshape(-1, 32)
+        G = len(cnt)
+        nsig = int((first + cnt).max()) if G else 0
+        gb = np.zeros((G + 7) // 8 + 1, np.uint8)
+        sb = np.zeros((nsig + 7) // 8 + 1, np.uint8)
+        _check(self.lib.nt_ed25519_verify_batch_groups(
+            self.ctx, _p(pk), _p(sig), _p(first, _u64p), _p(cnt, _u32p), _p(msg32), G, _p(gb),
+            _p(sb) if with_sig_bits else None), "nt_ed25519_verify_batch_groups")
+        if with_sig_bits:
+            return _unpack(gb, G), _unpack(sb, nsig)
+        return _unpack(gb, G)
+
+    def sign_batch(self, seeds, msg=None, off=None, ln=None):
+        seeds = _u8(seeds).reshape(-1, 32)
+        n = len(seeds)
+        pk = np.zeros((max(n, 1), 32), np.uint8)
+        if msg is None:
+            _check(self.lib.nt_ed25519_keypair_batch(self.ctx, _p(seeds), n, _p(pk)), "nt_ed25519_keypair_batch")
+            return pk[:n]
+        msg = _u8(msg) if len(msg) else np.zeros(1, np.uint8)
+        off = np.ascontiguousarray(off, np.uint64)
+        ln = np.ascontiguousarray(ln, np.uint64)
+        sig = np.zeros((max(n, 1), 64), np.uint8)
+        _check(self.lib.nt_ed25519_sign_batch(self.ctx, _p(seeds), _p(msg), _p(off, _u64p), _p(ln, _u64p), n,
+                                              _p(pk), _p(sig)), "nt_ed25519_sign_batch")
+        return pk[:n], sig[:n]
+
+    # ---- device-resident (torch tensors or raw pointers) ----
+    def dev_verify(self, dev, stream, mode, d_pk, d_sig, d_msg, d_off, d_len, n, d_out):
+        _check(self.lib.nt_dev_ed25519_verify(self.ctx, dev, stream, mode, d_pk, d_sig, d_msg, d_off, d_len,
+                                              n, d_out), "nt_dev_ed25519_verify")
+
+    def dev_sha512(self, dev, stream, d_data, d_off, d_len, n, d_out):
+        _check(self.lib.nt_dev_sha512_trunc32(self.ctx, dev, stream, d_data, d_off, d_len, n, d_out),
+               "nt_dev_sha512_trunc32")
+
+    def dev_sign(self, dev, stream, d_seed, d_msg, d_off, d_len, n, d_pk, d_sig):
+        _check(self.lib.nt_dev_ed25519_sign(self.ctx, dev, stream, d_seed, d_msg, d_off, d_len, n, d_pk, d_sig),
+               "nt_dev_ed25519_sign")
+
+    def dev_group_and(self, dev, stream, d_first, d_cnt, G, d_sig_words, d_group_words):
+        _check(self.lib.nt_dev_group_and(self.ctx, dev, stream, d_first, d_cnt, G, d_sig_words, d_group_words),
+               "nt_dev_group_and")
+
+
+_default = None
+
+
+def default_backend():
+    """Process-wide backend over all visible devices (created on first use)."""
+    global _default
+    if _default is None:
+        _default = Backend(0)
+    return _default

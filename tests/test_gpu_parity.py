@@ -1,0 +1,192 @@
+"""GPU parity: the gfx950 path through the C ABI vs. the golden fixtures and the
+CPU oracle (bit-exact digests, identical accept/reject decisions).
+"""
+import hashlib
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from _oracle import expand
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def be():
+    import ntcrypto
+    b = ntcrypto.Backend(0)
+    yield b
+    b.close()
+
+
+def _json(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+def _pack(msgs):
+    ln = np.array([len(m) for m in msgs], np.uint64)
+    off = np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.uint64)
+    return np.frombuffer(b"".join(msgs), np.uint8), off, ln
+
+
+# ------------------------------------------------------------------ SHA-512
+def test_sha512_golden_vectors(be):
+    v = _json("sha512_vectors.json")
+    msgs = [expand(e["label"].encode(), e["len"]) for e in v["vectors"]]
+    out = be.digest_many(msgs)
+    for e, d in zip(v["vectors"], out):
+        assert d.tobytes().hex() == e["digest512"][:64], e["len"]
+
+
+def test_sha512_reference_fixtures(be):
+    ref = _json("sha512_vectors.json")["reference_fixtures"]
+    rb = ref["real_batch_977x512"]
+    txs = [expand((rb["tx_label"] % i).encode(), rb["tx_len"]) for i in range(rb["ntx"])]
+    real = struct.pack("<IQ", 0, len(txs)) + b"".join(struct.pack("<Q", len(t)) + t for t in txs)
+    msgs = [bytes.fromhex(ref["processor_batch_228B"]["hex"]), b"Hello, world!", real,
+            expand(ref["buffer_500000"]["label"].encode(), 500000)]
+    out = be.digest_many(msgs)
+    assert out[0].tobytes().hex() == ref["processor_batch_228B"]["digest32"]
+    assert out[1].tobytes().hex() == ref["hello_world"]["digest32"]
+    assert out[2].tobytes().hex() == rb["digest32"]
+    assert out[3].tobytes().hex() == ref["buffer_500000"]["digest32"]
+
+
+def test_sha512_random_lengths_and_alignment(be):
+    rng = np.random.default_rng(11)
+    lens = np.concatenate([np.arange(0, 300), rng.integers(0, 20000, 200)]).astype(np.uint64)
+    gaps = rng.integers(0, 16, len(lens)).astype(np.uint64)  # arbitrary alignments
+    off = np.zeros(len(lens), np.uint64)
+    pos = 0
+    for i in range(len(lens)):
+        pos += int(gaps[i])
+        off[i] = pos
+        pos += int(lens[i])
+    data = rng.integers(0, 256, pos + 1, dtype=np.uint8)
+    out = be.sha512_trunc32(data, off, lens)
+    for i in range(len(lens)):
+        m = data[int(off[i]):int(off[i] + lens[i])].tobytes()
+        assert out[i].tobytes() == hashlib.sha512(m).digest()[:32], (i, int(lens[i]), int(off[i]))
+
+
+def test_sha512_empty_input(be):
+    out = be.sha512_trunc32(np.zeros(0, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint64))
+    assert out.shape == (0, 32)
+
+
+# ------------------------------------------------------------------ keygen / signing
+def test_keys_fixture_and_signatures(be):
+    ref = _json("fixtures_reference.json")
+    seeds = np.stack([np.frombuffer(bytes.fromhex(k["seed"]), np.uint8) for k in ref["keys"]])
+    d = bytes.fromhex(ref["hello_digest"])
+    data = np.frombuffer(d * 4, np.uint8)
+    pk, sig = be.sign_batch(seeds, data, np.arange(4, dtype=np.uint64) * 32, np.full(4, 32, np.uint64))
+    for i, k in enumerate(ref["keys"]):
+        assert pk[i].tobytes().hex() == k["pk"]
+        assert sig[i].tobytes().hex() == ref["hello_signatures"][i]
+
+
+def test_sign_matches_oracle_random(be, oracle):
+    rng = np.random.default_rng(5)
+    n = 300
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    msgs = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in rng.integers(0, 700, n)]
+    data, off, ln = _pack(msgs)
+    pk, sig = be.sign_batch(seeds, data, off, ln)
+    for i in range(n):
+        s = seeds[i].tobytes()
+        p = oracle.pubkey(s)
+        assert pk[i].tobytes() == p
+        assert sig[i].tobytes() == oracle.sign(s, p, msgs[i])
+
+
+# ------------------------------------------------------------------ verify_strict
+@pytest.fixture(scope="module")
+def corpus():
+    d = np.load(os.path.join(GOLD, "ed25519_corpus.npz"))
+    return {k: d[k] for k in d.files}
+
+
+def test_verify_strict_corpus(be, corpus):
+    got = be.verify_strict(corpus["pk"], corpus["sig"], corpus["msg"], corpus["off"], corpus["len"])
+    meta = _json("ed25519_corpus.json")
+    bad = [(i, meta["categories"][corpus["cat"][i]]) for i in np.nonzero(got != corpus["strict"].astype(bool))[0]]
+    assert not bad, bad[:20]
+
+
+def test_verify_strict_reference_tests(be):
+    """crypto_tests.rs:49-77 through the crate mirror."""
+    import ntcrypto as c
+    ref = _json("fixtures_reference.json")
+    k = ref["keys"][3]
+    pk = c.PublicKey(bytes.fromhex(k["pk"]))
+    sk = c.SecretKey(bytes.fromhex(k["seed"]) + bytes.fromhex(k["pk"]))
+    digest = c.sha512_digest(b"Hello, world!")
+    sig = c.Signature.new(digest, sk)
+    sig.verify(digest, pk)
+    with pytest.raises(c.CryptoError):
+        sig.verify(c.sha512_digest(b"Bad message!"), pk)
+
+
+def test_verify_strict_random_vs_oracle(be, oracle):
+    rng = np.random.default_rng(99)
+    n = 4096
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    msgs = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in rng.integers(0, 600, n)]
+    data, off, ln = _pack(msgs)
+    pk, sig = be.sign_batch(seeds, data, off, ln)
+    # corrupt a third of them in assorted ways
+    sig = sig.copy()
+    pk = pk.copy()
+    kind = rng.integers(0, 6, n)
+    for i in range(n):
+        if kind[i] == 1:
+            sig[i, rng.integers(0, 64)] ^= 1 << rng.integers(0, 8)
+        elif kind[i] == 2:
+            pk[i, rng.integers(0, 32)] ^= 1 << rng.integers(0, 8)
+    got = be.verify_strict(pk, sig, data, off, ln)
+    want = oracle.verify_strict_many(pk, sig, data, off, ln, nthreads=8).astype(bool)
+    assert np.array_equal(got, want)
+    assert got[kind != 1].sum() > 0
+
+
+def test_verify_empty(be):
+    got = be.verify_strict(np.zeros((0, 32), np.uint8), np.zeros((0, 64), np.uint8), np.zeros(0, np.uint8),
+                           np.zeros(0, np.uint64), np.zeros(0, np.uint64))
+    assert got.shape == (0,)
+
+
+# ------------------------------------------------------------------ verify_batch
+def test_batch_groups_fixture(be):
+    g = np.load(os.path.join(GOLD, "batch_groups.npz"))
+    gb, sb = be.verify_batch_groups(g["pk"], g["sig"], g["first"], g["cnt"], g["msg32"], with_sig_bits=True)
+    assert np.array_equal(gb, g["expect"].astype(bool))
+
+
+def test_batch_reference_tests():
+    """crypto_tests.rs:79-115 through the crate mirror."""
+    import ntcrypto as c
+    ref = _json("fixtures_reference.json")
+    digest = c.sha512_digest(b"Hello, world!")
+    keys = [(c.PublicKey(bytes.fromhex(k["pk"])), c.SecretKey(bytes.fromhex(k["seed"]) + bytes.fromhex(k["pk"])))
+            for k in ref["keys"]]
+    votes = [(pk, c.Signature.new(digest, sk)) for pk, sk in reversed(keys[1:])]
+    c.Signature.verify_batch(digest, votes)
+    bad = votes[:2] + [(keys[1][0], c.Signature.default())]
+    with pytest.raises(c.CryptoError):
+        c.Signature.verify_batch(digest, bad)
+
+
+def test_batch_corpus_rule(be, corpus):
+    """Each corpus entry as its own one-signature certificate (32-B messages only)."""
+    sel = np.nonzero(corpus["len"] == 32)[0]
+    pk = corpus["pk"][sel]
+    sig = corpus["sig"][sel]
+    msg32 = np.stack([corpus["msg"][int(corpus["off"][i]):int(corpus["off"][i]) + 32] for i in sel])
+    gb = be.verify_batch_groups(pk, sig, np.arange(len(sel), dtype=np.uint64), np.ones(len(sel), np.uint32), msg32)
+    assert np.array_equal(gb, corpus["batch_rule"][sel].astype(bool))
