@@ -1,0 +1,290 @@
+#!/usr/bin/env python3
+"""Benchmark of the Narwhal/Tusk crypto hot path on MI355X (gfx950).
+
+Metric (BASELINE.json): "Ed25519 verifies/sec + SHA-512 GB/s at 1/2/4/8 MI355X vs
+dalek host-core base".
+
+Headline line (`value`): BASELINE config 2 -- 1,000,000 independent
+verify_strict calls (crypto/src/lib.rs:200-204) over 512-byte messages with
+random keys and a 1 % edge-case mix (drawn from the
+committed golden corpus), inputs resident in HBM, per GPU (weak scaling: every
+rank verifies its own 1M).  A step = one verify launch over the 1M batch.
+
+Secondary (same JSON line, "sha512"): BASELINE config 4 -- SHA-512[..32] of
+16,384 x 500,000-byte batches (worker/src/processor.rs:38), GB/s.
+
+`roofline` is for the dominant kernel (k_ed25519_verify<strict>): it is an
+integer-VALU kernel, so achieved/peak are 32x32->64 multiply-accumulates per
+second (the algorithmic v_mad_u64_u32 count per verify)
+against the gfx950 issue peak of that instruction.
+
+`cpu_baseline`: the repo's CPU restatement (oracle/, radix-2^51 like the
+curve25519-dalek u64 backend) on a bounded sample of the same workload,
+rank 0 at N=1 only -- a reported baseline, also used as an in-bench parity
+check of the sample.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under
+torch.distributed.run (one process per GPU; gloo only for the barrier and the
+max-over-ranks timing -- the data path has no collective).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "narwhal-tusk_amd"))
+
+METRIC = "Ed25519 verifies/sec + SHA-512 GB/s at 1/2/4/8 MI355X vs dalek host-core base"
+MAD_PEAK_TS = 256 * 4 * 64 * 2.4e9 / 4 / 1e12  # v_mad_u64_u32: 4 cycles per wave64 per SIMD
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=1_000_000, help="signatures per GPU (config 2: 1M)")
+    ap.add_argument("--msg-len", type=int, default=512)
+    ap.add_argument("--sha-msgs", type=int, default=16384, help="config 4 messages (total, sharded)")
+    ap.add_argument("--sha-len", type=int, default=500_000)
+    ap.add_argument("--no-sha", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-seconds of baseline work")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import ntcrypto
+    be = ntcrypto.Backend(device=local)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    # ---------------------------------------------------------------- inputs (config 2)
+    n, L = args.n, args.msg_len
+    g = torch.Generator(device=dev)
+    g.manual_seed(20241220 + rank)
+    seeds = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device=dev, generator=g)
+    msgs = torch.randint(0, 256, (n * L + 64,), dtype=torch.uint8, device=dev, generator=g)
+    off = torch.arange(n, dtype=torch.int64, device=dev) * L
+    ln = torch.full((n,), L, dtype=torch.int64, device=dev)
+    pk = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    t0 = time.time()
+    be.dev_sign(0, sp, seeds.data_ptr(), msgs.data_ptr(), off.data_ptr(), ln.data_ptr(), n, pk.data_ptr(),
+                sig.data_ptr())
+    torch.cuda.synchronize(dev)
+    gen_s = time.time() - t0
+
+    # 1 % edge cases from the golden corpus (512-B entries), evenly over categories
+    corpus = np.load(os.path.join(ROOT, "tests", "golden", "ed25519_corpus.npz"))
+    meta = json.load(open(os.path.join(ROOT, "tests", "golden", "ed25519_corpus.json")))
+    pool = [i for i in range(len(corpus["cat"])) if int(corpus["len"][i]) == L
+            and meta["categories"][int(corpus["cat"][i])] != "honest"]
+    by_cat = {}
+    for i in pool:
+        by_cat.setdefault(int(corpus["cat"][i]), []).append(i)
+    cats = sorted(by_cat)
+    n_edge = n // 100
+    rng = np.random.default_rng(7 + rank)
+    pos = np.sort(rng.choice(n, size=n_edge, replace=False))
+    src = np.array([by_cat[cats[j % len(cats)]][(j // len(cats)) % len(by_cat[cats[j % len(cats)]])]
+                    for j in range(n_edge)], dtype=np.int64)
+    expect = np.ones(n, dtype=bool)
+    expect[pos] = corpus["strict"][src].astype(bool)
+    pk_h = pk.cpu().numpy()
+    sig_h = sig.cpu().numpy()
+    msg_h = msgs.cpu().numpy()
+    for p, s in zip(pos, src):
+        o = int(corpus["off"][s])
+        pk_h[p] = corpus["pk"][s]
+        sig_h[p] = corpus["sig"][s]
+        msg_h[p * L:(p + 1) * L] = corpus["msg"][o:o + L]
+    pk.copy_(torch.from_numpy(pk_h))
+    sig.copy_(torch.from_numpy(sig_h))
+    msgs.copy_(torch.from_numpy(msg_h))
+    words = (n + 63) // 64
+    out = torch.zeros(words, dtype=torch.int64, device=dev)
+
+    def step():
+        be.dev_verify(0, sp, ntcrypto.NT_MODE_STRICT, pk.data_ptr(), sig.data_ptr(), msgs.data_ptr(),
+                      off.data_ptr(), ln.data_ptr(), n, out.data_ptr())
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    barrier()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    wall = max_over_ranks(wall)
+    got = np.unpackbits(out.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+    mism = int((got != expect).sum())
+    mism = int(max_over_ranks(mism))
+
+    total = n * world * args.steps
+    value = total / wall
+    ms_per_step = wall * 1e3 / args.steps
+
+    # algorithmic multiply-accumulates per verify (counted by tests/cpp/opcount)
+    mads = mads_per_verify(L)
+    achieved = mads * n / (kernel_ms * 1e-3) / 1e12
+    prof = load_profile("r01_verify_pmc.json")
+    roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": round(MAD_PEAK_TS, 2),
+                "unit": "Tmad/s (v_mad_u64_u32 32x32->64 multiply-accumulates)",
+                "frac": round(achieved / MAD_PEAK_TS, 4),
+                "traffic": prof.get("hbm_bytes_per_launch") if prof else None,
+                "kernel": "k_ed25519_verify<strict>", "kernel_ms": round(kernel_ms, 3),
+                "mads_per_verify": mads}
+
+    line = {"metric": METRIC, "value": round(value, 1), "unit": "verifies/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 limbs / u64 acc",
+            "data": "synthetic (seeded random keys and 512-B messages, GPU-signed; 1% Appendix-B edge cases "
+                    "from tests/golden/ed25519_corpus.npz)",
+            "config": {"workload": "cfg2: 1M verify_strict per GPU, 512-B messages, 1% edge mix",
+                       "n_per_gpu": n, "msg_len": L, "edge_cases": n_edge,
+                       "parallelism": "shard-by-index, one process per GPU, no collective"},
+            "roofline": roofline,
+            "parity": {"mismatches_vs_expected": mism, "checked": n * world},
+            "input_gen_s": round(gen_s, 3)}
+
+    # ---------------------------------------------------------------- config 4: SHA-512 GB/s
+    if not args.no_sha:
+        line["sha512"] = bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_ranks)
+
+    # ---------------------------------------------------------------- CPU baseline (rank 0, N=1)
+    if world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(args, pk_h, sig_h, msg_h, L, got)
+
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    be.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_ranks):
+    m_total, ml = args.sha_msgs, args.sha_len
+    m = (m_total + world - 1) // world  # this rank's shard of the 16,384 messages
+    m = min(m, m_total - rank * m) if rank * m < m_total else 0
+    g = torch.Generator(device=dev)
+    g.manual_seed(4242 + rank)
+    data = torch.randint(0, 256, (m * ml + 64,), dtype=torch.uint8, device=dev, generator=g)
+    off = torch.arange(m, dtype=torch.int64, device=dev) * ml
+    ln = torch.full((m,), ml, dtype=torch.int64, device=dev)
+    out = torch.empty((m, 32), dtype=torch.uint8, device=dev)
+
+    def step():
+        be.dev_sha512(0, sp, data.data_ptr(), off.data_ptr(), ln.data_ptr(), m, out.data_ptr())
+
+    steps = max(1, min(args.steps, 5))
+    for _ in range(max(1, args.warmup)):
+        step()
+    barrier()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        step()
+    ev1.record(stream)
+    barrier()
+    wall = max_over_ranks(time.perf_counter() - t0)
+    kms = ev0.elapsed_time(ev1) / steps
+    # spot-check 4 digests against hashlib
+    import hashlib
+    ok = True
+    idx = [0, m // 3, (2 * m) // 3, m - 1] if m else []
+    for i in idx:
+        b = data[i * ml:(i + 1) * ml].cpu().numpy().tobytes()
+        ok &= hashlib.sha512(b).digest()[:32] == out[i].cpu().numpy().tobytes()
+    padded = (ml + 17 + 127) // 128 * 128
+    gbs = m_total * ml / wall * steps / 1e9 if wall > 0 else 0.0
+    return {"value": round(gbs, 2), "unit": "GB/s (message bytes)", "workload": "cfg4: %d x %d B" % (m_total, ml),
+            "ms_per_step": round(wall * 1e3 / steps, 3), "kernel_ms": round(kms, 3),
+            "hbm_frac": round((m * padded / (kms * 1e-3)) / 1e9 / HBM_PEAK_GBS, 4),
+            "note": "one lane per message: 16,384 lanes = 256 waves, latency-bound (SURVEY H2)",
+            "spot_check_ok": bool(ok)}
+
+
+def cpu_baseline(args, pk_h, sig_h, msg_h, L, got):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle
+    orc = _oracle.load()
+    th = args.cpu_threads
+    # calibrate: per-verify cost on one thread
+    k = 256
+    offs = (np.arange(k, dtype=np.uint64) * L)
+    lens = np.full(k, L, np.uint64)
+    t0 = time.perf_counter()
+    orc.verify_strict_many(pk_h[:k], sig_h[:k], msg_h[:k * L], offs, lens, nthreads=1)
+    per = (time.perf_counter() - t0) / k
+    sample = int(min(len(pk_h), max(th * 64, args.cpu_seconds / per)))
+    offs = (np.arange(sample, dtype=np.uint64) * L)
+    lens = np.full(sample, L, np.uint64)
+    t0 = time.perf_counter()
+    res = orc.verify_strict_many(pk_h[:sample], sig_h[:sample], msg_h[:sample * L], offs, lens, nthreads=th)
+    dt = time.perf_counter() - t0
+    agree = int((res.astype(bool) == got[:sample]).sum())
+    return {"value": round(sample / dt, 1), "unit": "verifies/s", "cores": th, "kind": "port",
+            "sample": "first %d of the same 1M cfg2 verifies (%.1f s wall on %d threads)" % (sample, dt, th),
+            "single_thread_us_per_verify": round(per * 1e6, 2),
+            "verdicts_agree_with_gpu": "%d/%d" % (agree, sample)}
+
+
+def mads_per_verify(msg_len):
+    path = os.path.join(ROOT, "profiles", "opcount.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return int(d["verify_strict_mads"])
+    except Exception:
+        return None
+
+
+def load_profile(name):
+    try:
+        with open(os.path.join(ROOT, "profiles", name)) as f:
+            return json.load(f)
+    except Exception:
+        return None
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,216 @@
+// ed25519_ops.hpp -- per-lane Ed25519 operations shared by the gfx950 kernels
+// (kernels.hip) and the host-compiled bound/op-count harness (tools/opcount.cpp,
+// tests/cpp/).  Table storage is abstracted:
+//   ATab: store(entry, ge_cached) / load(entry, ge_cached&)   -- j*(-A), j = 0..8
+//   BTab: load(idx, ge_niels&)                                 -- j*B,   j = 0..128
+//
+// Semantics (restated from ed25519-dalek 1.0.1 /
+// curve25519-dalek 3.x):
+//   verify_one<kStrict>       = PublicKey::verify_strict  (crypto/src/lib.rs:200-204)
+//   verify_one<kCofactorless> = one entry of verify_batch under the deterministic
+//                               rule A.3                   (crypto/src/lib.rs:206-219)
+//   sign_one                  = Keypair::generate + sign   (crypto/src/lib.rs:163-191)
+#pragma once
+#include "fe25519.hpp"
+#include "ge25519.hpp"
+#include "sc25519.hpp"
+#include "sha512.hpp"
+
+namespace nt {
+
+// [j]B as an affine-niels entry (j = 0 -> identity).
+NT_HD NT_INLINE void btab_entry(ge_niels& q, uint32_t j) {
+  if (j == 0) {
+    ge_niels_0(q);
+    return;
+  }
+  uint32_t enc[8];
+  for (int i = 0; i < 8; ++i) enc[i] = kBaseEnc[i];
+  ge_p3 B, P;
+  ge_frombytes_w(B, enc);
+  ge_cached Bc;
+  ge_p3_to_cached(Bc, B);
+  ge_p3_0(P);
+  for (int bit = 7; bit >= 0; --bit) {
+    ge_p2 t2;
+    ge_cp t;
+    ge_p3_to_p2(t2, P);
+    ge_dbl(t, t2);
+    ge_cp_to_p3(P, t);
+    if ((j >> bit) & 1) {
+      ge_add_cached(t, P, Bc);
+      ge_cp_to_p3(P, t);
+    }
+  }
+  fe zi, x, y, d2;
+  fe_invert(zi, P.Z);
+  fe_mul(x, P.X, zi);
+  fe_mul(y, P.Y, zi);
+  fe_add(q.ypx, y, x);
+  fe_carry(q.ypx);
+  fe_sub(q.ymx, y, x);
+  fe_carry(q.ymx);
+  fe_const(d2, kFeD2);
+  fe_mul(q.xy2d, x, y);
+  fe_mul(q.xy2d, q.xy2d, d2);
+}
+
+// acc = [s]B + [k](-A): 64 signed 4-bit windows of k, 32 signed 8-bit windows of s.
+// Every lane follows the same schedule (no divergence).
+template <class ATab, class BTab>
+NT_HD NT_INLINE void ladder(ge_p2& acc, const uint32_t kd[8], const uint32_t sd[8], const ATab& at,
+                            const BTab& bt) {
+  uint32_t kw[8], sw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { kw[i] = kd[i]; sw[i] = sd[i]; }
+  ge_p2_0(acc);
+  ge_cp t;
+  ge_p3 u;
+  for (int wi = 7; wi >= 0; --wi) {
+    const uint32_t kcur = kw[7], scur = sw[7];
+#pragma unroll
+    for (int m = 7; m > 0; --m) { kw[m] = kw[m - 1]; sw[m] = sw[m - 1]; }
+    for (int j = 7; j >= 0; --j) {
+      for (int r = 0; r < 3; ++r) ge_dbl_p2(acc, acc);
+      ge_dbl(t, acc);
+      ge_cp_to_p3(u, t);
+      const int32_t dk = (int32_t)(((kcur >> (4 * j)) & 15u) ^ 8u) - 8;
+      const uint32_t negk = dk < 0;
+      ge_cached ce;
+      at.load((uint32_t)(negk ? -dk : dk), ce);
+      ge_cached_cneg(ce, negk);
+      ge_add_cached(t, u, ce);
+      if ((j & 1) == 0) {
+        const int32_t ds = (int32_t)(((scur >> (4 * j)) & 255u) ^ 128u) - 128;
+        const uint32_t negs = ds < 0;
+        ge_niels ne;
+        bt.load((uint32_t)(negs ? -ds : ds), ne);
+        ge_niels_cneg(ne, negs);
+        ge_cp_to_p3(u, t);
+        ge_add_niels(t, u, ne);
+      }
+      ge_cp_to_p2(acc, t);
+    }
+  }
+}
+
+// Fixed-base [x]B (x < L) with 8-bit signed windows.
+template <class BTab>
+NT_HD NT_INLINE void base_mul(ge_p2& acc, const uint32_t x[8], const BTab& bt) {
+  uint32_t sd[8];
+  sc_recode_w8(sd, x);
+  ge_p2_0(acc);
+  ge_cp t;
+  ge_p3 u;
+  for (int wi = 7; wi >= 0; --wi) {
+    const uint32_t scur = sd[7];
+#pragma unroll
+    for (int m = 7; m > 0; --m) sd[m] = sd[m - 1];
+    for (int j = 3; j >= 0; --j) {
+      for (int r = 0; r < 7; ++r) ge_dbl_p2(acc, acc);
+      ge_dbl(t, acc);
+      ge_cp_to_p3(u, t);
+      const int32_t ds = (int32_t)(((scur >> (8 * j)) & 255u) ^ 128u) - 128;
+      const uint32_t negs = ds < 0;
+      ge_niels ne;
+      bt.load((uint32_t)(negs ? -ds : ds), ne);
+      ge_niels_cneg(ne, negs);
+      ge_add_niels(t, u, ne);
+      ge_cp_to_p2(acc, t);
+    }
+  }
+}
+
+// One verification. Aw = pk words, Rw/Sw = signature halves, msg/len = message.
+template <int MODE, class ATab, class BTab>
+NT_HD NT_INLINE uint32_t verify_one(const uint32_t Aw[8], const uint32_t Rw[8], const uint32_t Sw[8],
+                                    const uint8_t* msg, uint64_t len, ATab& at, const BTab& bt) {
+  const uint32_t s_ok = sc_is_canonical(Sw);
+  ge_p3 A, R;
+  const uint32_t a_ok = ge_frombytes_w(A, Aw);
+  const uint32_t r_ok = ge_frombytes_w(R, Rw);
+  uint32_t small = 0;
+  if (MODE == kStrict) small = ge_is_small_order(A) | ge_is_small_order(R);
+
+  // k = SHA-512(R || A || M) mod L over the raw encodings (Scalar::from_hash)
+  uint32_t prefix[16];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) { prefix[q] = Rw[q]; prefix[8 + q] = Aw[q]; }
+  uint64_t st[8];
+  sha512_prefixed<16>(st, prefix, msg, len);
+  uint32_t hw[16], k[8];
+  sha512_out_words(hw, st, 16);
+  sc_reduce512(k, hw);
+
+  // table j * (-A), j = 0..8
+  ge_p3 An;
+  fe_neg(An.X, A.X);
+  fe_carry(An.X);
+  An.Y = A.Y;
+  An.Z = A.Z;
+  fe_neg(An.T, A.T);
+  fe_carry(An.T);
+  {
+    ge_cached c0, c1;
+    ge_cached_0(c0);
+    at.store(0, c0);
+    ge_p3_to_cached(c1, An);
+    at.store(1, c1);
+    ge_p3 cur = An;
+    for (uint32_t j = 2; j < 9; ++j) {
+      ge_cp t;
+      ge_add_cached(t, cur, c1);
+      ge_cp_to_p3(cur, t);
+      ge_cached cj;
+      ge_p3_to_cached(cj, cur);
+      at.store(j, cj);
+    }
+  }
+
+  uint32_t kd[8], sd[8];
+  sc_recode_w4(kd, k);
+  sc_recode_w8(sd, Sw);
+  ge_p2 Rp;
+  ladder(Rp, kd, sd, at, bt);
+  const uint32_t eq = ge_eq_affine(Rp, R);
+  return s_ok & a_ok & r_ok & (small ^ 1u) & eq;
+}
+
+// Keygen + RFC 8032 signature.  sw = 32-byte seed words.
+template <class BTab>
+NT_HD NT_INLINE void sign_one(uint32_t Aw[8], uint32_t Rw[8], uint32_t s[8], const uint32_t sw[8],
+                              const uint8_t* msg, uint64_t len, const BTab& bt) {
+  uint64_t st[8];
+  sha512_prefixed<8>(st, sw, nullptr, 0);
+  uint32_t h[16];
+  sha512_out_words(h, st, 16);
+  uint32_t a[8], pre[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) { a[q] = h[q]; pre[q] = h[8 + q]; }
+  a[0] &= 0xfffffff8u;
+  a[7] &= 0x3fffffffu;
+  a[7] |= 0x40000000u;
+  uint32_t ared[8];
+  sc_reduce256(ared, a);
+  ge_p2 P;
+  base_mul(P, ared, bt);
+  ge_tobytes_w(Aw, P);
+
+  sha512_prefixed<8>(st, pre, msg, len);
+  uint32_t hr[16], r[8];
+  sha512_out_words(hr, st, 16);
+  sc_reduce512(r, hr);
+  base_mul(P, r, bt);
+  ge_tobytes_w(Rw, P);
+
+  uint32_t prefix[16];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) { prefix[q] = Rw[q]; prefix[8 + q] = Aw[q]; }
+  sha512_prefixed<16>(st, prefix, msg, len);
+  uint32_t hk[16], k[8];
+  sha512_out_words(hk, st, 16);
+  sc_reduce512(k, hk);
+  sc_muladd(s, k, a, r);
+}
+
+}  // namespace nt

@@ -14,11 +14,21 @@
 //   "R"  reduced   : output of mul/sq/carry: even limbs < 2^26, odd < 2^25 (+2^18 on limb 1)
 //   mul(f, g)      : f limbs < 2^28.6 (odd limbs get x2), g limbs < 2^27.75 (get x19)
 //                    => each term < 2^60.4, 10 terms < 2^63.8 < 2^64
-//   sq(f)          : f limbs < 2^27.75
+//   sq(f)          : f limbs < 2^27 (4f x 19f terms, <= 6 per column => < 2^62.8)
 //   sub(f,g)       : f + 2p - g, needs g "R" (or sub4: f + 4p - g, g < 2^27 even / 2^26 odd)
 // Every point formula in ge25519.hpp is annotated with the bound it relies on.
 #pragma once
 #include "nt_common.hpp"
+
+#if defined(NT_OPCOUNT) && !defined(__HIP_DEVICE_COMPILE__)
+// Host-only instrumentation (tools/opcount.cpp): counts field multiplies.
+namespace nt { extern unsigned long long g_fe_mul, g_fe_sq; }
+#define NT_COUNT_MUL() (++::nt::g_fe_mul)
+#define NT_COUNT_SQ() (++::nt::g_fe_sq)
+#else
+#define NT_COUNT_MUL() ((void)0)
+#define NT_COUNT_SQ() ((void)0)
+#endif
 
 namespace nt {
 
@@ -112,6 +122,7 @@ NT_HD NT_INLINE void fe_carry_wide(fe& out, uint64_t h[10]) {
 
 // h = f * g.  Each partial product is one v_mad_u64_u32.
 NT_HD NT_INLINE void fe_mul(fe& out, const fe& f, const fe& g) {
+  NT_COUNT_MUL();
   uint32_t g19[10], f2[10];
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
@@ -138,6 +149,7 @@ NT_HD NT_INLINE void fe_mul(fe& out, const fe& f, const fe& g) {
 
 // h = f^2 using the symmetric products (55 instead of 100 multiplies).
 NT_HD NT_INLINE void fe_sq(fe& out, const fe& f) {
+  NT_COUNT_SQ();
   uint32_t f2[10], f4[10], f19[10];
 #pragma unroll
   for (int i = 0; i < 10; ++i) {

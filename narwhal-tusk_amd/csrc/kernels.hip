@@ -19,11 +19,8 @@
 // each lane's 16-byte accesses coalesce across the workgroup.
 #include <hip/hip_runtime.h>
 
-#include "fe25519.hpp"
-#include "ge25519.hpp"
+#include "ed25519_ops.hpp"
 #include "kernels.hpp"
-#include "sc25519.hpp"
-#include "sha512.hpp"
 
 namespace nt {
 
@@ -52,9 +49,14 @@ __global__ __launch_bounds__(kBlock) void k_sha512_trunc32(const uint8_t* __rest
 }
 
 // --------------------------------------------------------------------------
-// Base-point table
+// Base-point table: one thread per entry j = 0..128
 // --------------------------------------------------------------------------
-NT_D NT_INLINE void store_niels(uint32_t* dst, const ge_niels& q) {
+__global__ void k_btab_init(uint32_t* __restrict__ tab) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= kBEntries) return;
+  ge_niels q;
+  btab_entry(q, (uint32_t)j);
+  uint32_t* dst = tab + (size_t)j * kBStride;
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
     dst[i] = q.ypx.v[i];
@@ -65,165 +67,68 @@ NT_D NT_INLINE void store_niels(uint32_t* dst, const ge_niels& q) {
   dst[31] = 0;
 }
 
-__global__ void k_btab_init(uint32_t* __restrict__ tab) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= kBEntries) return;
-  ge_niels q;
-  if (j == 0) {
-    ge_niels_0(q);
-    store_niels(tab, q);
-    return;
-  }
-  uint32_t enc[8];
+// --------------------------------------------------------------------------
+// Table accessors
+// --------------------------------------------------------------------------
+// [j]B entries staged in LDS, 32 words per entry (8 x ds_read_b128).
+struct LdsBTab {
+  const uint32_t* lds;
+  NT_D NT_INLINE void load(uint32_t idx, ge_niels& q) const {
+    const uint4* e = (const uint4*)(lds + idx * kBStride);
+    uint32_t w[32];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) enc[i] = kBaseEnc[i];
-  ge_p3 B, P;
-  ge_frombytes_w(B, enc);
-  ge_cached Bc;
-  ge_p3_to_cached(Bc, B);
-  ge_p3_0(P);
-  for (int bit = 7; bit >= 0; --bit) {
-    ge_p2 t2;
-    ge_cp t;
-    ge_p3_to_p2(t2, P);
-    ge_dbl(t, t2);
-    ge_cp_to_p3(P, t);
-    if ((j >> bit) & 1) {
-      ge_add_cached(t, P, Bc);
-      ge_cp_to_p3(P, t);
+    for (int i = 0; i < 8; ++i) {
+      const uint4 v = e[i];
+      w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      q.ypx.v[i] = w[i];
+      q.ymx.v[i] = w[10 + i];
+      q.xy2d.v[i] = w[20 + i];
     }
   }
-  fe zi, x, y, d2;
-  fe_invert(zi, P.Z);
-  fe_mul(x, P.X, zi);
-  fe_mul(y, P.Y, zi);
-  fe_add(q.ypx, y, x);
-  fe_carry(q.ypx);
-  fe_sub(q.ymx, y, x);
-  fe_carry(q.ymx);
-  fe_const(d2, kFeD2);
-  fe_mul(q.xy2d, x, y);
-  fe_mul(q.xy2d, q.xy2d, d2);
-  store_niels(tab + (size_t)j * kBStride, q);
-}
+};
 
-// --------------------------------------------------------------------------
-// Table access helpers
-// --------------------------------------------------------------------------
-NT_D NT_INLINE void lds_load_niels(ge_niels& q, const uint32_t* btab, uint32_t idx) {
-  const uint4* e = (const uint4*)(btab + idx * kBStride);
-  uint32_t w[32];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint4 v = e[i];
-    w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+// j*(-A) entries in the global workspace, layout [slot][entry][quad][lane] of
+// uint4: a lane's 16-byte accesses are adjacent to its neighbours'.
+struct WsATab {
+  uint4* ws;
+  uint32_t slot;
+  NT_D NT_INLINE uint4* at(uint32_t entry) const {
+    return ws + ((size_t)(slot * kAEntries + entry) * kAQuads) * kBlock + threadIdx.x;
   }
+  NT_D NT_INLINE void store(uint32_t entry, const ge_cached& c) const {
+    uint32_t w[40];
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    q.ypx.v[i] = w[i];
-    q.ymx.v[i] = w[10 + i];
-    q.xy2d.v[i] = w[20 + i];
+    for (int i = 0; i < 10; ++i) {
+      w[i] = c.YpX.v[i]; w[10 + i] = c.YmX.v[i]; w[20 + i] = c.Z2.v[i]; w[30 + i] = c.T2d.v[i];
+    }
+    uint4* base = at(entry);
+#pragma unroll
+    for (int q = 0; q < kAQuads; ++q)
+      base[(size_t)q * kBlock] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
   }
-}
-
-// workspace: [slot][entry][quad][lane] of uint4
-NT_D NT_INLINE void ws_store_cached(uint4* ws, uint32_t slot, uint32_t entry, const ge_cached& c) {
-  uint32_t w[40];
+  NT_D NT_INLINE void load(uint32_t entry, ge_cached& c) const {
+    uint32_t w[40];
+    const uint4* base = at(entry);
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    w[i] = c.YpX.v[i]; w[10 + i] = c.YmX.v[i]; w[20 + i] = c.Z2.v[i]; w[30 + i] = c.T2d.v[i];
+    for (int q = 0; q < kAQuads; ++q) {
+      const uint4 v = base[(size_t)q * kBlock];
+      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      c.YpX.v[i] = w[i]; c.YmX.v[i] = w[10 + i]; c.Z2.v[i] = w[20 + i]; c.T2d.v[i] = w[30 + i];
+    }
   }
-  uint4* base = ws + ((size_t)(slot * kAEntries + entry) * kAQuads) * kBlock + threadIdx.x;
-#pragma unroll
-  for (int q = 0; q < kAQuads; ++q)
-    base[(size_t)q * kBlock] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-}
-
-NT_D NT_INLINE void ws_load_cached(ge_cached& c, const uint4* ws, uint32_t slot, uint32_t entry) {
-  uint32_t w[40];
-  const uint4* base = ws + ((size_t)(slot * kAEntries + entry) * kAQuads) * kBlock + threadIdx.x;
-#pragma unroll
-  for (int q = 0; q < kAQuads; ++q) {
-    const uint4 v = base[(size_t)q * kBlock];
-    w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
-  }
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    c.YpX.v[i] = w[i]; c.YmX.v[i] = w[10 + i]; c.Z2.v[i] = w[20 + i]; c.T2d.v[i] = w[30 + i];
-  }
-}
+};
 
 NT_D NT_INLINE void load_btab_lds(uint32_t* lds, const uint32_t* __restrict__ btab_g) {
   const uint4* src = (const uint4*)btab_g;
   uint4* dst = (uint4*)lds;
   for (int i = threadIdx.x; i < kBEntries * kBStride / 4; i += kBlock) dst[i] = src[i];
   __syncthreads();
-}
-
-// --------------------------------------------------------------------------
-// Double-scalar ladder:  acc = [s]B + [k]Aneg   (4-bit k windows, 8-bit s windows)
-// --------------------------------------------------------------------------
-NT_D NT_INLINE void ladder(ge_p2& acc, const uint32_t kd[8], const uint32_t sd[8], const uint4* ws,
-                           uint32_t slot, const uint32_t* btab) {
-  uint32_t kw[8], sw[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) { kw[i] = kd[i]; sw[i] = sd[i]; }
-  ge_p2_0(acc);
-  ge_cp t;
-  ge_p3 u;
-  for (int wi = 7; wi >= 0; --wi) {
-    const uint32_t kcur = kw[7], scur = sw[7];
-#pragma unroll
-    for (int m = 7; m > 0; --m) { kw[m] = kw[m - 1]; sw[m] = sw[m - 1]; }
-    for (int j = 7; j >= 0; --j) {
-      for (int r = 0; r < 3; ++r) ge_dbl_p2(acc, acc);
-      ge_dbl(t, acc);
-      ge_cp_to_p3(u, t);
-      // k digit: two's-complement nibble
-      const int32_t dk = (int32_t)(((kcur >> (4 * j)) & 15u) ^ 8u) - 8;
-      const uint32_t negk = dk < 0;
-      ge_cached ce;
-      ws_load_cached(ce, ws, slot, (uint32_t)(negk ? -dk : dk));
-      ge_cached_cneg(ce, negk);
-      ge_add_cached(t, u, ce);
-      if ((j & 1) == 0) {
-        const int32_t ds = (int32_t)(((scur >> (4 * j)) & 255u) ^ 128u) - 128;
-        const uint32_t negs = ds < 0;
-        ge_niels ne;
-        lds_load_niels(ne, btab, (uint32_t)(negs ? -ds : ds));
-        ge_niels_cneg(ne, negs);
-        ge_cp_to_p3(u, t);
-        ge_add_niels(t, u, ne);
-      }
-      ge_cp_to_p2(acc, t);
-    }
-  }
-}
-
-// Fixed-base [x]B with 8-bit windows (x < L), used for keygen and signing.
-NT_D NT_INLINE void base_mul(ge_p2& acc, const uint32_t x[8], const uint32_t* btab) {
-  uint32_t sd[8];
-  sc_recode_w8(sd, x);
-  ge_p2_0(acc);
-  ge_cp t;
-  ge_p3 u;
-  for (int wi = 7; wi >= 0; --wi) {
-    const uint32_t scur = sd[7];
-#pragma unroll
-    for (int m = 7; m > 0; --m) sd[m] = sd[m - 1];
-    for (int j = 3; j >= 0; --j) {
-      for (int r = 0; r < 7; ++r) ge_dbl_p2(acc, acc);
-      ge_dbl(t, acc);
-      ge_cp_to_p3(u, t);
-      const int32_t ds = (int32_t)(((scur >> (8 * j)) & 255u) ^ 128u) - 128;
-      const uint32_t negs = ds < 0;
-      ge_niels ne;
-      lds_load_niels(ne, btab, (uint32_t)(negs ? -ds : ds));
-      ge_niels_cneg(ne, negs);
-      ge_add_niels(t, u, ne);
-      ge_cp_to_p2(acc, t);
-    }
-  }
 }
 
 NT_D NT_INLINE void load8(uint32_t w[8], const uint32_t* __restrict__ p) {
@@ -233,7 +138,7 @@ NT_D NT_INLINE void load8(uint32_t w[8], const uint32_t* __restrict__ p) {
 }
 
 // --------------------------------------------------------------------------
-// Verification
+// Verification: one lane per signature, grid-stride over workspace slots
 // --------------------------------------------------------------------------
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_ed25519_verify(
@@ -243,67 +148,17 @@ __global__ __launch_bounds__(kBlock) void k_ed25519_verify(
     unsigned long long* __restrict__ out_bits) {
   __shared__ __attribute__((aligned(16))) uint32_t btab[kBEntries * kBStride];
   load_btab_lds(btab, btab_g);
-  const uint32_t slot = blockIdx.x;
+  const LdsBTab bt{btab};
+  WsATab at{ws, blockIdx.x};
   for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < n; base += (uint64_t)gridDim.x * kBlock) {
     const uint64_t gi = base + threadIdx.x;
     const uint32_t active = gi < n;
     const uint64_t i = active ? gi : n - 1;
-
     uint32_t Aw[8], Rw[8], Sw[8];
     load8(Aw, pk + 8 * i);
     load8(Rw, sig + 16 * i);
     load8(Sw, sig + 16 * i + 8);
-
-    const uint32_t s_ok = sc_is_canonical(Sw);
-    ge_p3 A, R;
-    const uint32_t a_ok = ge_frombytes_w(A, Aw);
-    const uint32_t r_ok = ge_frombytes_w(R, Rw);
-    uint32_t small = 0;
-    if (MODE == kStrict) small = ge_is_small_order(A) | ge_is_small_order(R);
-
-    // k = H(R || A || M) mod L over the raw encodings
-    uint32_t prefix[16];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) { prefix[q] = Rw[q]; prefix[8 + q] = Aw[q]; }
-    uint64_t st[8];
-    sha512_prefixed<16>(st, prefix, msg + off[i], len[i]);
-    uint32_t hw[16], k[8];
-    sha512_out_words(hw, st, 16);
-    sc_reduce512(k, hw);
-
-    // table of j * (-A), j = 0..8
-    ge_p3 An;
-    fe_neg(An.X, A.X);
-    fe_carry(An.X);
-    An.Y = A.Y;
-    An.Z = A.Z;
-    fe_neg(An.T, A.T);
-    fe_carry(An.T);
-    {
-      ge_cached c0, c1;
-      ge_cached_0(c0);
-      ws_store_cached(ws, slot, 0, c0);
-      ge_p3_to_cached(c1, An);
-      ws_store_cached(ws, slot, 1, c1);
-      ge_p3 cur = An;
-      for (uint32_t j = 2; j < kAEntries; ++j) {
-        ge_cp t;
-        ge_add_cached(t, cur, c1);
-        ge_cp_to_p3(cur, t);
-        ge_cached cj;
-        ge_p3_to_cached(cj, cur);
-        ws_store_cached(ws, slot, j, cj);
-      }
-    }
-
-    uint32_t kd[8], sd[8];
-    sc_recode_w4(kd, k);
-    sc_recode_w8(sd, Sw);
-    ge_p2 Rp;
-    ladder(Rp, kd, sd, ws, slot, btab);
-    const uint32_t eq = ge_eq_affine(Rp, R);
-
-    const uint32_t ok = active & s_ok & a_ok & r_ok & (small ^ 1u) & eq;
+    const uint32_t ok = active & verify_one<MODE>(Aw, Rw, Sw, msg + off[i], len[i], at, bt);
     const unsigned long long bal = __ballot(ok);
     const uint64_t wbase = base + (threadIdx.x & ~63u);
     if ((threadIdx.x & 63u) == 0 && wbase < n) out_bits[wbase >> 6] = bal;
@@ -348,47 +203,17 @@ __global__ __launch_bounds__(kBlock) void k_ed25519_sign(const uint32_t* __restr
                                                         uint32_t* __restrict__ out_sig) {
   __shared__ __attribute__((aligned(16))) uint32_t btab[kBEntries * kBStride];
   load_btab_lds(btab, btab_g);
+  const LdsBTab bt{btab};
   for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < n; base += (uint64_t)gridDim.x * kBlock) {
     const uint64_t gi = base + threadIdx.x;
     const uint32_t active = gi < n;
     const uint64_t i = active ? gi : n - 1;
     uint32_t sw[8];
     load8(sw, seed + 8 * i);
-    uint64_t st[8];
-    sha512_prefixed<8>(st, sw, nullptr, 0);
-    uint32_t h[16];
-    sha512_out_words(h, st, 16);
-    uint32_t a[8], pre[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) { a[q] = h[q]; pre[q] = h[8 + q]; }
-    a[0] &= 0xfffffff8u;
-    a[7] &= 0x3fffffffu;
-    a[7] |= 0x40000000u;
-    uint32_t ared[8];
-    sc_reduce256(ared, a);
-    ge_p2 P;
-    base_mul(P, ared, btab);
-    uint32_t Aw[8];
-    ge_tobytes_w(Aw, P);
-
+    uint32_t Aw[8], Rw[8], s[8];
     const uint8_t* m = msg ? msg + off[i] : nullptr;
     const uint64_t ml = msg ? len[i] : 0;
-    sha512_prefixed<8>(st, pre, m, ml);
-    uint32_t hr[16], r[8];
-    sha512_out_words(hr, st, 16);
-    sc_reduce512(r, hr);
-    base_mul(P, r, btab);
-    uint32_t Rw[8];
-    ge_tobytes_w(Rw, P);
-
-    uint32_t prefix[16];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) { prefix[q] = Rw[q]; prefix[8 + q] = Aw[q]; }
-    sha512_prefixed<16>(st, prefix, m, ml);
-    uint32_t hk[16], k[8], s[8];
-    sha512_out_words(hk, st, 16);
-    sc_reduce512(k, hk);
-    sc_muladd(s, k, a, r);
+    sign_one(Aw, Rw, s, sw, m, ml, bt);
     if (active) {
       uint4* po = (uint4*)(out_pk + 8 * i);
       po[0] = make_uint4(Aw[0], Aw[1], Aw[2], Aw[3]);
@@ -408,7 +233,7 @@ __global__ __launch_bounds__(kBlock) void k_ed25519_sign(const uint32_t* __restr
 // Launchers (host)
 // --------------------------------------------------------------------------
 hipError_t launch_btab_init(uint32_t* d_tab, hipStream_t s) {
-  hipLaunchKernelGGL(k_btab_init, dim3(3), dim3(64), 0, s, d_tab);
+  hipLaunchKernelGGL(k_btab_init, dim3((kBEntries + 63) / 64), dim3(64), 0, s, d_tab);
   return hipGetLastError();
 }
 

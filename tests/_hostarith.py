@@ -1,0 +1,91 @@
+"""ctypes binding of tests/cpp/build/libnthost.so -- the device arithmetic compiled
+for the host (TEST INFRASTRUCTURE; see tests/cpp/nt_host_harness.cpp)."""
+import ctypes
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CPP = os.path.join(ROOT, "tests", "cpp")
+LIB = os.path.join(CPP, "build", "libnthost.so")
+SH = [26, 25] * 5
+W = [sum(SH[:i]) for i in range(10)]
+P = 2 ** 255 - 19
+L = 2 ** 252 + 27742317777372353535851937790883648493
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        subprocess.run(["make", "-s", "-C", CPP], check=True)
+        _lib = ctypes.CDLL(LIB)
+        _lib.nth_verify.restype = ctypes.c_int
+        _lib.nth_count_mul.restype = ctypes.c_ulonglong
+        _lib.nth_count_sq.restype = ctypes.c_ulonglong
+    return _lib
+
+
+def arr(limbs):
+    return (ctypes.c_uint32 * 10)(*limbs)
+
+
+def value(limbs):
+    return sum(int(l) << w for l, w in zip(limbs, W))
+
+
+def to_limbs(x):
+    out = []
+    for s in SH:
+        out.append(x & ((1 << s) - 1))
+        x >>= s
+    return out
+
+
+def fe_mul(f, g):
+    o = (ctypes.c_uint32 * 10)()
+    load().nth_fe_mul(arr(f), arr(g), o)
+    return list(o)
+
+
+def fe_sq(f):
+    o = (ctypes.c_uint32 * 10)()
+    load().nth_fe_sq(arr(f), o)
+    return list(o)
+
+
+def fe_tobytes(f):
+    o = ctypes.create_string_buffer(32)
+    load().nth_fe_tobytes(arr(f), o)
+    return o.raw
+
+
+def verify(mode, pk, sig, msg):
+    return bool(load().nth_verify(mode, pk, sig, msg, ctypes.c_uint64(len(msg))))
+
+
+def sign(seed, msg):
+    pk = ctypes.create_string_buffer(32)
+    sig = ctypes.create_string_buffer(64)
+    load().nth_sign(seed, msg, ctypes.c_uint64(len(msg)), pk, sig)
+    return pk.raw, sig.raw
+
+
+def sc_reduce512(b):
+    o = ctypes.create_string_buffer(32)
+    load().nth_sc_reduce512(b, o)
+    return o.raw
+
+
+def sha512(m):
+    o = ctypes.create_string_buffer(64)
+    load().nth_sha512(m, ctypes.c_uint64(len(m)), o)
+    return o.raw
+
+
+def counts_reset():
+    load().nth_counts_reset()
+
+
+def counts():
+    return int(load().nth_count_mul()), int(load().nth_count_sq())
