@@ -74,8 +74,12 @@ def main():
 
     import ntcrypto
     be = ntcrypto.Backend(device=local)
-    stream = torch.cuda.current_stream(dev)
+    # a real (non-null) stream: the library launches on it and the HIP events
+    # bracketing the timed region are recorded on it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
+    assert sp != 0
 
     def barrier():
         torch.cuda.synchronize(dev)

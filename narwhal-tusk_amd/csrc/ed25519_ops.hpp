@@ -66,11 +66,14 @@ NT_HD NT_INLINE void ladder(ge_p2& acc, const uint32_t kd[8], const uint32_t sd[
   ge_p2_0(acc);
   ge_cp t;
   ge_p3 u;
+#pragma unroll 1
   for (int wi = 7; wi >= 0; --wi) {
     const uint32_t kcur = kw[7], scur = sw[7];
 #pragma unroll
     for (int m = 7; m > 0; --m) { kw[m] = kw[m - 1]; sw[m] = sw[m - 1]; }
+#pragma unroll 1
     for (int j = 7; j >= 0; --j) {
+#pragma unroll 1
       for (int r = 0; r < 3; ++r) ge_dbl_p2(acc, acc);
       ge_dbl(t, acc);
       ge_cp_to_p3(u, t);
@@ -102,11 +105,14 @@ NT_HD NT_INLINE void base_mul(ge_p2& acc, const uint32_t x[8], const BTab& bt) {
   ge_p2_0(acc);
   ge_cp t;
   ge_p3 u;
+#pragma unroll 1
   for (int wi = 7; wi >= 0; --wi) {
     const uint32_t scur = sd[7];
 #pragma unroll
     for (int m = 7; m > 0; --m) sd[m] = sd[m - 1];
+#pragma unroll 1
     for (int j = 3; j >= 0; --j) {
+#pragma unroll 1
       for (int r = 0; r < 7; ++r) ge_dbl_p2(acc, acc);
       ge_dbl(t, acc);
       ge_cp_to_p3(u, t);
@@ -122,41 +128,31 @@ NT_HD NT_INLINE void base_mul(ge_p2& acc, const uint32_t x[8], const BTab& bt) {
 }
 
 // One verification. Aw = pk words, Rw/Sw = signature halves, msg/len = message.
+// Order chosen to keep little state live across the ladder: A is decoded and
+// checked first; R is only decoded after the ladder (its bytes are 8 words).
 template <int MODE, class ATab, class BTab>
 NT_HD NT_INLINE uint32_t verify_one(const uint32_t Aw[8], const uint32_t Rw[8], const uint32_t Sw[8],
                                     const uint8_t* msg, uint64_t len, ATab& at, const BTab& bt) {
-  const uint32_t s_ok = sc_is_canonical(Sw);
-  ge_p3 A, R;
-  const uint32_t a_ok = ge_frombytes_w(A, Aw);
-  const uint32_t r_ok = ge_frombytes_w(R, Rw);
-  uint32_t small = 0;
-  if (MODE == kStrict) small = ge_is_small_order(A) | ge_is_small_order(R);
-
-  // k = SHA-512(R || A || M) mod L over the raw encodings (Scalar::from_hash)
-  uint32_t prefix[16];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) { prefix[q] = Rw[q]; prefix[8 + q] = Aw[q]; }
-  uint64_t st[8];
-  sha512_prefixed<16>(st, prefix, msg, len);
-  uint32_t hw[16], k[8];
-  sha512_out_words(hw, st, 16);
-  sc_reduce512(k, hw);
-
-  // table j * (-A), j = 0..8
-  ge_p3 An;
-  fe_neg(An.X, A.X);
-  fe_carry(An.X);
-  An.Y = A.Y;
-  An.Z = A.Z;
-  fe_neg(An.T, A.T);
-  fe_carry(An.T);
+  uint32_t ok = sc_is_canonical(Sw);
   {
+    ge_p3 A;
+    ok &= ge_frombytes_w(A, Aw);
+    if (MODE == kStrict) ok &= ge_is_small_order(A) ^ 1u;
+    // table j * (-A), j = 0..8
+    ge_p3 An;
+    fe_neg(An.X, A.X);
+    fe_carry(An.X);
+    An.Y = A.Y;
+    An.Z = A.Z;
+    fe_neg(An.T, A.T);
+    fe_carry(An.T);
     ge_cached c0, c1;
     ge_cached_0(c0);
     at.store(0, c0);
     ge_p3_to_cached(c1, An);
     at.store(1, c1);
     ge_p3 cur = An;
+#pragma unroll 1
     for (uint32_t j = 2; j < 9; ++j) {
       ge_cp t;
       ge_add_cached(t, cur, c1);
@@ -166,14 +162,27 @@ NT_HD NT_INLINE uint32_t verify_one(const uint32_t Aw[8], const uint32_t Rw[8], 
       at.store(j, cj);
     }
   }
-
   uint32_t kd[8], sd[8];
-  sc_recode_w4(kd, k);
-  sc_recode_w8(sd, Sw);
+  {
+    // k = SHA-512(R || A || M) mod L over the raw encodings (Scalar::from_hash)
+    uint32_t prefix[16];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { prefix[q] = Rw[q]; prefix[8 + q] = Aw[q]; }
+    uint64_t st[8];
+    sha512_prefixed<16>(st, prefix, msg, len);
+    uint32_t hw[16], k[8];
+    sha512_out_words(hw, st, 16);
+    sc_reduce512(k, hw);
+    sc_recode_w4(kd, k);
+    sc_recode_w8(sd, Sw);
+  }
   ge_p2 Rp;
   ladder(Rp, kd, sd, at, bt);
-  const uint32_t eq = ge_eq_affine(Rp, R);
-  return s_ok & a_ok & r_ok & (small ^ 1u) & eq;
+  ge_p3 R;
+  ok &= ge_frombytes_w(R, Rw);
+  if (MODE == kStrict) ok &= ge_is_small_order(R) ^ 1u;
+  ok &= ge_eq_affine(Rp, R);
+  return ok;
 }
 
 // Keygen + RFC 8032 signature.  sw = 32-byte seed words.

@@ -30,6 +30,15 @@ namespace nt { extern unsigned long long g_fe_mul, g_fe_sq; }
 #define NT_COUNT_SQ() ((void)0)
 #endif
 
+// Scheduling fence after each multiply: the 10 column chains inside one mul
+// are enough ILP for a wave; letting the scheduler overlap several muls only
+// multiplies register pressure (spills, lower occupancy).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(NT_NO_MUL_FENCE)
+#define NT_MUL_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define NT_MUL_FENCE() ((void)0)
+#endif
+
 namespace nt {
 
 struct fe {
@@ -145,6 +154,7 @@ NT_HD NT_INLINE void fe_mul(fe& out, const fe& f, const fe& g) {
     h[k] = acc;
   }
   fe_carry_wide(out, h);
+  NT_MUL_FENCE();
 }
 
 // h = f^2 using the symmetric products (55 instead of 100 multiplies).
@@ -175,10 +185,14 @@ NT_HD NT_INLINE void fe_sq(fe& out, const fe& f) {
     }
   }
   fe_carry_wide(out, h);
+  NT_MUL_FENCE();
 }
 
+// Repeated squaring; kept as a loop (not unrolled) so the exponentiation chains
+// stay small in the instruction cache.
 NT_HD NT_INLINE void fe_sqn(fe& out, const fe& f, int n) {
   fe_sq(out, f);
+#pragma unroll 1
   for (int i = 1; i < n; ++i) fe_sq(out, out);
 }
 

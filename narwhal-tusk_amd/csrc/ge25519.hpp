@@ -202,9 +202,8 @@ NT_HD NT_INLINE uint32_t ge_p2_is_identity(const ge_p2& p) {
 NT_HD NT_INLINE uint32_t ge_is_small_order(const ge_p3& p) {
   ge_p2 t;
   ge_p3_to_p2(t, p);
-  ge_dbl_p2(t, t);
-  ge_dbl_p2(t, t);
-  ge_dbl_p2(t, t);
+#pragma unroll 1
+  for (int i = 0; i < 3; ++i) ge_dbl_p2(t, t);
   return ge_p2_is_identity(t);
 }
 

@@ -19,6 +19,8 @@
 // each lane's 16-byte accesses coalesce across the workgroup.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "ed25519_ops.hpp"
 #include "kernels.hpp"
 
@@ -140,8 +142,8 @@ NT_D NT_INLINE void load8(uint32_t w[8], const uint32_t* __restrict__ p) {
 // --------------------------------------------------------------------------
 // Verification: one lane per signature, grid-stride over workspace slots
 // --------------------------------------------------------------------------
-template <int MODE>
-__global__ __launch_bounds__(kBlock) void k_ed25519_verify(
+template <int MODE, int OCC>
+__global__ __launch_bounds__(kBlock, OCC) void k_ed25519_verify(
     const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t n,
     const uint32_t* __restrict__ btab_g, uint4* __restrict__ ws,
@@ -246,6 +248,32 @@ hipError_t launch_sha512_trunc32(const uint8_t* d_data, const uint64_t* d_off, c
   return hipGetLastError();
 }
 
+// Occupancy variant of the verify kernel (waves per SIMD the register
+// allocator targets): 1 = no spills, 2 = twice the latency hiding with some
+// scratch.  NT_VERIFY_OCC selects at run time (A/B measurement); default 2.
+static int verify_occ() {
+  static int occ = [] {
+    const char* e = std::getenv("NT_VERIFY_OCC");
+    return (e && std::atoi(e) == 1) ? 1 : 2;
+  }();
+  return occ;
+}
+
+template <int MODE>
+static void launch_verify_mode(uint64_t blocks, const uint8_t* d_pk, const uint8_t* d_sig,
+                               const uint8_t* d_msg, const uint64_t* d_off, const uint64_t* d_len,
+                               uint64_t n, const uint32_t* d_btab, void* d_ws, uint64_t* d_out_words,
+                               hipStream_t s) {
+  if (verify_occ() == 1)
+    hipLaunchKernelGGL((k_ed25519_verify<MODE, 1>), dim3((uint32_t)blocks), dim3(kBlock), 0, s,
+                       (const uint32_t*)d_pk, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_btab,
+                       (uint4*)d_ws, (unsigned long long*)d_out_words);
+  else
+    hipLaunchKernelGGL((k_ed25519_verify<MODE, 2>), dim3((uint32_t)blocks), dim3(kBlock), 0, s,
+                       (const uint32_t*)d_pk, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_btab,
+                       (uint4*)d_ws, (unsigned long long*)d_out_words);
+}
+
 hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
                          const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
                          const uint32_t* d_btab, void* d_ws, uint32_t ws_slots, uint64_t* d_out_words,
@@ -254,13 +282,10 @@ hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, co
   uint64_t blocks = (n + kBlock - 1) / kBlock;
   if (blocks > ws_slots) blocks = ws_slots;
   if (mode == kStrict)
-    hipLaunchKernelGGL(k_ed25519_verify<kStrict>, dim3((uint32_t)blocks), dim3(kBlock), 0, s,
-                       (const uint32_t*)d_pk, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_btab,
-                       (uint4*)d_ws, (unsigned long long*)d_out_words);
+    launch_verify_mode<kStrict>(blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_btab, d_ws, d_out_words, s);
   else
-    hipLaunchKernelGGL(k_ed25519_verify<kCofactorless>, dim3((uint32_t)blocks), dim3(kBlock), 0, s,
-                       (const uint32_t*)d_pk, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_btab,
-                       (uint4*)d_ws, (unsigned long long*)d_out_words);
+    launch_verify_mode<kCofactorless>(blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_btab, d_ws,
+                                      d_out_words, s);
   return hipGetLastError();
 }
 

@@ -15,11 +15,7 @@
 
 namespace nt {
 
-#if defined(__HIP_DEVICE_COMPILE__)
-__constant__ static const uint64_t kSha512K[80] = {
-#else
-static const uint64_t kSha512K[80] = {
-#endif
+static constexpr uint64_t kSha512K[80] = {
     0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
     0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
     0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
@@ -41,7 +37,50 @@ static const uint64_t kSha512K[80] = {
     0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
     0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
 
-NT_HD NT_INLINE uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+NT_HD NT_INLINE uint64_t rotr64_generic(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+// 64-bit rotate / shift by a constant as two v_alignbit_b32 (the compiler's own
+// lowering used shift/shift/or sequences: ~2x the instructions).
+template <int N>
+NT_HD NT_INLINE uint64_t rotr64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  uint32_t rlo, rhi;
+  if constexpr (N < 32) {
+    rlo = __builtin_amdgcn_alignbit(hi, lo, N);
+    rhi = __builtin_amdgcn_alignbit(lo, hi, N);
+  } else {
+    rlo = __builtin_amdgcn_alignbit(lo, hi, N - 32);
+    rhi = __builtin_amdgcn_alignbit(hi, lo, N - 32);
+  }
+  return ((uint64_t)rhi << 32) | rlo;
+#else
+  return rotr64_generic(x, N);
+#endif
+}
+template <int N>
+NT_HD NT_INLINE uint64_t shr64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return ((uint64_t)(hi >> N) << 32) | __builtin_amdgcn_alignbit(hi, lo, N);
+#else
+  return x >> N;
+#endif
+}
+// Maj(a,b,c) = bfi(a^b, c, b): one xor + one v_bfi_b32 per half
+NT_HD NT_INLINE uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) {
+  const uint64_t m = a ^ b;
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t lo, hi;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(lo) : "v"((uint32_t)m), "v"((uint32_t)c), "v"((uint32_t)b));
+  asm("v_bfi_b32 %0, %1, %2, %3"
+      : "=v"(hi)
+      : "v"((uint32_t)(m >> 32)), "v"((uint32_t)(c >> 32)), "v"((uint32_t)(b >> 32)));
+  return ((uint64_t)hi << 32) | lo;
+#else
+  return (m & c) | (~m & b);
+#endif
+}
 
 NT_HD NT_INLINE uint32_t bswap32(uint32_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -58,15 +97,55 @@ NT_HD NT_INLINE void sha512_init(uint64_t st[8]) {
   st[6] = 0x1f83d9abfb41bd6bULL; st[7] = 0x5be0cd19137e2179ULL;
 }
 
-#define NT_SHA_ROUND(a, b, c, d, e, f, g, h, kw)                                   \
-  {                                                                                \
-    const uint64_t t1 = h + (rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41)) +      \
-                        ((e & f) ^ (~e & g)) + (kw);                               \
-    const uint64_t t2 = (rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39)) +          \
-                        ((a & b) ^ (a & c) ^ (b & c));                             \
-    d += t1;                                                                       \
-    h = t1 + t2;                                                                   \
+// Round constant K as an SGPR pair materialized at its use.  A plain constant
+// is hoisted out of the block loop by LICM into 160 VGPRs (80 x 64-bit),
+// which is what drove the first build of this kernel to 256 VGPRs.  The
+// volatile asm cannot be hoisted, costs two SALU slots per round and no VGPR.
+template <int R>
+NT_HD NT_INLINE uint64_t sha_k() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t lo, hi;
+  asm volatile("s_mov_b32 %0, %2\n\ts_mov_b32 %1, %3"
+               : "=s"(lo), "=s"(hi)
+               : "i"((uint32_t)kSha512K[R]), "i"((uint32_t)(kSha512K[R] >> 32)));
+  return ((uint64_t)hi << 32) | lo;
+#else
+  return kSha512K[R];
+#endif
+}
+
+template <int R>
+NT_HD NT_INLINE void sha_round(uint64_t v[8], uint64_t W[16]) {
+  // working variables rotate by index instead of by moves
+  uint64_t& a = v[(8 - R % 8) % 8];
+  uint64_t& b = v[(9 - R % 8) % 8];
+  uint64_t& c = v[(10 - R % 8) % 8];
+  uint64_t& d = v[(11 - R % 8) % 8];
+  uint64_t& e = v[(12 - R % 8) % 8];
+  uint64_t& f = v[(13 - R % 8) % 8];
+  uint64_t& g = v[(14 - R % 8) % 8];
+  uint64_t& h = v[(15 - R % 8) % 8];
+  if constexpr (R >= 16) {
+    constexpr int i = R & 15;
+    const uint64_t w15 = W[(i + 1) & 15], w2 = W[(i + 14) & 15];
+    const uint64_t s0 = rotr64<1>(w15) ^ rotr64<8>(w15) ^ shr64<7>(w15);
+    const uint64_t s1 = rotr64<19>(w2) ^ rotr64<61>(w2) ^ shr64<6>(w2);
+    W[i] += s0 + W[(i + 9) & 15] + s1;
   }
+  const uint64_t t1 = h + (rotr64<14>(e) ^ rotr64<18>(e) ^ rotr64<41>(e)) + ((e & f) | (~e & g)) +
+                      sha_k<R>() + W[R & 15];
+  const uint64_t t2 = (rotr64<28>(a) ^ rotr64<34>(a) ^ rotr64<39>(a)) + maj64(a, b, c);
+  d += t1;
+  h = t1 + t2;
+}
+
+template <int R>
+NT_HD NT_INLINE void sha_rounds(uint64_t v[8], uint64_t W[16]) {
+  if constexpr (R < 80) {
+    sha_round<R>(v, W);
+    sha_rounds<R + 1>(v, W);
+  }
+}
 
 // One compression. blk[i] = LE 32-bit words of the 128-byte block as stored in memory.
 NT_HD NT_INLINE void sha512_compress_words(uint64_t st[8], const uint32_t blk[32]) {
@@ -74,29 +153,12 @@ NT_HD NT_INLINE void sha512_compress_words(uint64_t st[8], const uint32_t blk[32
 #pragma unroll
   for (int t = 0; t < 16; ++t)
     W[t] = ((uint64_t)bswap32(blk[2 * t]) << 32) | bswap32(blk[2 * t + 1]);
-  uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+  uint64_t v[8];
 #pragma unroll
-  for (int r = 0; r < 80; r += 8) {
-    if (r >= 16) {
+  for (int i = 0; i < 8; ++i) v[i] = st[i];
+  sha_rounds<0>(v, W);
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int i = (r + t) & 15;
-        const uint64_t w15 = W[(i + 1) & 15], w2 = W[(i + 14) & 15];
-        const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-        const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
-        W[i] += s0 + W[(i + 9) & 15] + s1;
-      }
-    }
-    NT_SHA_ROUND(a, b, c, d, e, f, g, h, kSha512K[r + 0] + W[(r + 0) & 15]);
-    NT_SHA_ROUND(h, a, b, c, d, e, f, g, kSha512K[r + 1] + W[(r + 1) & 15]);
-    NT_SHA_ROUND(g, h, a, b, c, d, e, f, kSha512K[r + 2] + W[(r + 2) & 15]);
-    NT_SHA_ROUND(f, g, h, a, b, c, d, e, kSha512K[r + 3] + W[(r + 3) & 15]);
-    NT_SHA_ROUND(e, f, g, h, a, b, c, d, kSha512K[r + 4] + W[(r + 4) & 15]);
-    NT_SHA_ROUND(d, e, f, g, h, a, b, c, kSha512K[r + 5] + W[(r + 5) & 15]);
-    NT_SHA_ROUND(c, d, e, f, g, h, a, b, kSha512K[r + 6] + W[(r + 6) & 15]);
-    NT_SHA_ROUND(b, c, d, e, f, g, h, a, kSha512K[r + 7] + W[(r + 7) & 15]);
-  }
-  st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+  for (int i = 0; i < 8; ++i) st[i] += v[i];
 }
 
 // Load NW little-endian words starting at byte address p (any alignment) from
@@ -134,6 +196,49 @@ NT_HD NT_INLINE void load_words(uint32_t* w, const uint8_t* p) {
   }
 }
 
+// Tail block b (not made only of message bytes): message bytes, 0x80, zeros
+// and -- in the last block -- the 128-bit big-endian bit length.  Only 4-byte
+// granules that contain message bytes are read (predicated aligned loads).
+template <int PW>
+NT_HD NT_INLINE void sha512_tail_block(uint32_t blk[32], const uint32_t* prefix, const uint8_t* msg,
+                                       uint64_t len, uint64_t b, bool last) {
+  const uint64_t total = (uint64_t)(4 * PW) + len;
+  const uintptr_t base = (uintptr_t)msg;
+  const uint32_t sh = (uint32_t)(base & 3u);
+  const uint32_t* pw = (const uint32_t*)(base & ~(uintptr_t)3);
+  const uint64_t mend = (uint64_t)sh + len;  // message end relative to pw (bytes)
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const uint64_t pos = 128 * b + 4 * i;  // stream position of this word
+    if (i < PW && b == 0) {
+      blk[i] = prefix[i < PW ? i : 0];
+      continue;
+    }
+    // message-relative byte offset of the word (pos >= 4*PW here)
+    const uint64_t r = pos - 4 * PW;
+    const uint64_t g0 = (r + sh) >> 2;  // aligned granule holding the first byte
+    const uint32_t lo = (4 * g0 < mend) ? pw[g0] : 0u;
+    const uint32_t hi = (sh != 0 && 4 * (g0 + 1) < mend) ? pw[g0 + 1] : 0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, sh);
+#else
+    uint32_t w = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * sh));
+#endif
+    // keep bytes < len, put 0x80 at byte len, zero the rest
+    const uint64_t have = (len > r) ? (len - r) : 0;  // message bytes in this word
+    const uint32_t keep = have >= 4 ? 0xffffffffu : ((1u << (8 * (uint32_t)have)) - 1u);
+    const uint32_t pad = (pos <= total && total < pos + 4) ? (0x80u << (8 * (uint32_t)(total - pos))) : 0u;
+    blk[i] = (w & keep) | pad;
+  }
+  if (last) {
+    const uint64_t bits = total << 3;
+    blk[28] = 0;
+    blk[29] = bswap32((uint32_t)(total >> 61));
+    blk[30] = bswap32((uint32_t)(bits >> 32));
+    blk[31] = bswap32((uint32_t)bits);
+  }
+}
+
 // Hash  prefix[0..PW) || msg[0..len)  and return the 8 state words.
 template <int PW>
 NT_HD NT_INLINE void sha512_prefixed(uint64_t st[8], const uint32_t* prefix, const uint8_t* msg,
@@ -143,45 +248,22 @@ NT_HD NT_INLINE void sha512_prefixed(uint64_t st[8], const uint32_t* prefix, con
   const uint64_t nblocks = (total + 17 + 127) / 128;
   const uint64_t nfull = total / 128;  // blocks made only of prefix/message bytes
   uint32_t blk[32];
-  for (uint64_t b = 0; b < nblocks; ++b) {
-    if (b < nfull) {
-      if (b == 0) {
+  uint64_t b = 0;
+  if (PW > 0 && nfull > 0) {
 #pragma unroll
-        for (int i = 0; i < PW; ++i) blk[i] = prefix[i];
-        load_words<32 - PW>(blk + PW, msg);
-      } else {
-        load_words<32>(blk, msg + (128 * b - 4 * PW));
-      }
-    } else {
-      // tail block(s): bytes beyond the message, 0x80, zeros, 128-bit length
-#pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        uint32_t wv = 0;
-        if (i < PW && b == 0) {
-          wv = prefix[i < PW ? i : 0];  // prefix words are whole words of block 0
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const uint64_t pos = 128 * b + 4 * i + j;  // position in the stream
-            uint32_t byte;
-            if (pos < total) {
-              byte = msg[pos - 4 * PW];
-            } else {
-              byte = (pos == total) ? 0x80u : 0u;
-            }
-            wv |= byte << (8 * j);
-          }
-        }
-        blk[i] = wv;
-      }
-      if (b == nblocks - 1) {
-        const uint64_t bits = total << 3;
-        blk[28] = 0;
-        blk[29] = bswap32((uint32_t)(total >> 61));
-        blk[30] = bswap32((uint32_t)(bits >> 32));
-        blk[31] = bswap32((uint32_t)bits);
-      }
-    }
+    for (int i = 0; i < PW; ++i) blk[i] = prefix[i];
+    load_words<32 - PW>(blk + PW, msg);
+    sha512_compress_words(st, blk);
+    b = 1;
+  }
+#pragma unroll 1
+  for (; b < nfull; ++b) {
+    load_words<32>(blk, msg + (128 * b - 4 * PW));
+    sha512_compress_words(st, blk);
+  }
+#pragma unroll 1
+  for (; b < nblocks; ++b) {
+    sha512_tail_block<PW>(blk, prefix, msg, len, b, b == nblocks - 1);
     sha512_compress_words(st, blk);
   }
 }
