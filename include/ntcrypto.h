@@ -95,6 +95,28 @@ int nt_ed25519_sign_batch(nt_ctx *ctx, const uint8_t *seed32, const uint8_t *msg
                           uint8_t *sig64);
 int nt_ed25519_keypair_batch(nt_ctx *ctx, const uint8_t *seed32, uint64_t n, uint8_t *pk32);
 
+/* ---- committee key cache ------------------------------
+ * A keyset holds, on every device of the context, per-key comb tables
+ * (32 x 129 affine multiples of -A, 528 KiB per key) plus each key's raw
+ * encoding and decode / small-order flags, so verification against a static
+ * committee (config/src/lib.rs:140-143) needs no decompression of A and no
+ * doublings.  Keys are addressed by index (the caller's committee order);
+ * an index >= nkeys means "not a committee key" and verifies as reject.
+ * Keys that do not decode are accepted into the set and always reject, as
+ * PublicKey::from_bytes would (crypto/src/lib.rs:202,216). */
+typedef struct nt_keyset nt_keyset;
+int nt_keyset_create(nt_ctx *ctx, const uint8_t *pk32, uint32_t nkeys, nt_keyset **out);
+void nt_keyset_free(nt_keyset *ks);
+/* flags of key i: bit 0 = decodes, bit 1 = small order */
+int nt_keyset_flags(const nt_keyset *ks, uint32_t i, uint32_t *flags);
+int nt_ed25519_verify_keyset(nt_ctx *ctx, const nt_keyset *ks, int mode, const uint32_t *key_idx,
+                             const uint8_t *sig64, const uint8_t *msg, const uint64_t *off,
+                             const uint64_t *len, uint64_t n, uint8_t *out_bitmap);
+int nt_ed25519_verify_batch_groups_keyset(nt_ctx *ctx, const nt_keyset *ks, const uint32_t *key_idx,
+                                          const uint8_t *sig64, const uint64_t *first,
+                                          const uint32_t *cnt, const uint8_t *msg32, uint64_t G,
+                                          uint8_t *out_group_bitmap, uint8_t *out_sig_bitmap);
+
 /* ---- device-resident entry points (enqueue only) ---------------------- */
 int nt_dev_sha512_trunc32(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_data,
                           const uint64_t *d_off, const uint64_t *d_len, uint64_t n,
@@ -106,6 +128,10 @@ int nt_dev_ed25519_verify(nt_ctx *ctx, int dev, void *stream, int mode, const ui
 int nt_dev_group_and(nt_ctx *ctx, int dev, void *stream, const uint64_t *d_first,
                      const uint32_t *d_cnt, uint64_t G, const uint64_t *d_sig_words,
                      uint64_t *d_group_words);
+int nt_dev_ed25519_verify_keyset(nt_ctx *ctx, const nt_keyset *ks, int dev, void *stream, int mode,
+                                 const uint32_t *d_key_idx, const uint8_t *d_sig64,
+                                 const uint8_t *d_msg, const uint64_t *d_off, const uint64_t *d_len,
+                                 uint64_t n, uint64_t *d_out_words);
 int nt_dev_ed25519_sign(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_seed32,
                         const uint8_t *d_msg, const uint64_t *d_off, const uint64_t *d_len,
                         uint64_t n, uint8_t *d_pk32, uint8_t *d_sig64);

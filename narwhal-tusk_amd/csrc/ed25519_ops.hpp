@@ -223,3 +223,114 @@ NT_HD NT_INLINE void sign_one(uint32_t Aw[8], uint32_t Rw[8], uint32_t s[8], con
 }
 
 }  // namespace nt
+
+namespace nt {
+
+// ---------------------------------------------------------------------------
+// Committee key cache: fixed-base combs.
+//   comb entry (i, j) = j * 256^i * P  as affine niels, i in [0, 32), j in [0, 128]
+// With a comb for -A and one for B, [s]B + [k](-A) is 64 mixed additions and
+// no doublings: 32 signed 8-bit digits of k and of s.
+// ---------------------------------------------------------------------------
+constexpr int kCombPos = 32;
+constexpr int kCombEntries = 129;
+
+// j * 256^i * P (P given as p3), returned affine-niels.
+NT_HD NT_INLINE void comb_entry(ge_niels& q, const ge_p3& P, uint32_t i, uint32_t j) {
+  if (j == 0) {
+    ge_niels_0(q);
+    return;
+  }
+  ge_cached Pc;
+  ge_p3_to_cached(Pc, P);
+  ge_p3 Q;
+  ge_p3_0(Q);
+  ge_cp t;
+#pragma unroll 1
+  for (int bit = 7; bit >= 0; --bit) {
+    ge_p2 t2;
+    ge_p3_to_p2(t2, Q);
+    ge_dbl(t, t2);
+    ge_cp_to_p3(Q, t);
+    if ((j >> bit) & 1) {
+      ge_add_cached(t, Q, Pc);
+      ge_cp_to_p3(Q, t);
+    }
+  }
+  ge_p2 q2;
+  ge_p3_to_p2(q2, Q);
+#pragma unroll 1
+  for (uint32_t r = 0; r < 8 * i; ++r) ge_dbl_p2(q2, q2);
+  fe zi, x, y, d2;
+  fe_invert(zi, q2.Z);
+  fe_mul(x, q2.X, zi);
+  fe_mul(y, q2.Y, zi);
+  fe_add(q.ypx, y, x);
+  fe_carry(q.ypx);
+  fe_sub(q.ymx, y, x);
+  fe_carry(q.ymx);
+  fe_const(d2, kFeD2);
+  fe_mul(q.xy2d, x, y);
+  fe_mul(q.xy2d, q.xy2d, d2);
+}
+
+// Key metadata bits produced at keyset build time.
+enum : uint32_t { kKeyDecodes = 1u, kKeySmallOrder = 2u };
+
+// One verification against a cached key.  CA: comb of -A, CB: comb of B;
+// both expose load(pos, idx, ge_niels&).  meta: kKey* bits of the key.
+template <int MODE, class CombA, class CombB>
+NT_HD NT_INLINE uint32_t verify_one_cached(uint32_t meta, const uint32_t Aw[8], const uint32_t Rw[8],
+                                           const uint32_t Sw[8], const uint8_t* msg, uint64_t len,
+                                           const CombA& ca, const CombB& cb) {
+  uint32_t ok = sc_is_canonical(Sw) & (meta & kKeyDecodes ? 1u : 0u);
+  if (MODE == kStrict) ok &= (meta & kKeySmallOrder) ? 0u : 1u;
+  uint32_t kd[8], sd[8];
+  {
+    uint32_t prefix[16];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { prefix[q] = Rw[q]; prefix[8 + q] = Aw[q]; }
+    uint64_t st[8];
+    sha512_prefixed<16>(st, prefix, msg, len);
+    uint32_t hw[16], k[8];
+    sha512_out_words(hw, st, 16);
+    sc_reduce512(k, hw);
+    sc_recode_w8(kd, k);
+    sc_recode_w8(sd, Sw);
+  }
+  ge_p3 acc;
+  ge_p3_0(acc);
+  ge_cp t;
+  // word w of kd/sd holds the digits of positions 4w..4w+3 (one byte each);
+  // consume word 0 and shift the arrays down (no dynamic register indexing)
+#pragma unroll 1
+  for (int w = 0; w < 8; ++w) {
+    const uint32_t kw = kd[0], sw = sd[0];
+#pragma unroll
+    for (int m = 0; m < 7; ++m) { kd[m] = kd[m + 1]; sd[m] = sd[m + 1]; }
+#pragma unroll 1
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t pos = 4 * w + b;
+      const int32_t dk = (int32_t)(((kw >> (8 * b)) & 255u) ^ 128u) - 128;
+      const int32_t ds = (int32_t)(((sw >> (8 * b)) & 255u) ^ 128u) - 128;
+      ge_niels ne;
+      ca.load(pos, (uint32_t)(dk < 0 ? -dk : dk), ne);
+      ge_niels_cneg(ne, dk < 0);
+      ge_add_niels(t, acc, ne);
+      ge_cp_to_p3(acc, t);
+      cb.load(pos, (uint32_t)(ds < 0 ? -ds : ds), ne);
+      ge_niels_cneg(ne, ds < 0);
+      ge_add_niels(t, acc, ne);
+      ge_cp_to_p3(acc, t);
+    }
+  }
+  ge_p3 R;
+  ok &= ge_frombytes_w(R, Rw);
+  if (MODE == kStrict) ok &= ge_is_small_order(R) ^ 1u;
+  ge_p2 Rp;
+  ge_p3_to_p2(Rp, acc);
+  ok &= ge_eq_affine(Rp, R);
+  return ok;
+}
+
+}  // namespace nt

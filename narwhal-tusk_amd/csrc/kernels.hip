@@ -168,6 +168,92 @@ __global__ __launch_bounds__(kBlock, OCC) void k_ed25519_verify(
 }
 
 // --------------------------------------------------------------------------
+// Committee key cache: comb tables  [pos][key][entry][32 words]
+// --------------------------------------------------------------------------
+// One thread per (key, pos, entry).  sign_neg = 1 builds the comb of -P (keys),
+// 0 the comb of P itself (the base point).  meta[key] gets kKey* bits.
+__global__ void k_comb_build(const uint32_t* __restrict__ enc, uint32_t nkeys, int negate,
+                             uint32_t* __restrict__ comb, uint32_t* __restrict__ meta) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t per_key = (uint64_t)kCombPos * kCombEntries;
+  if (t >= per_key * nkeys) return;
+  const uint32_t key = (uint32_t)(t / per_key);
+  const uint32_t pos = (uint32_t)((t % per_key) / kCombEntries);
+  const uint32_t j = (uint32_t)(t % kCombEntries);
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = enc[8 * key + i];
+  ge_p3 P;
+  const uint32_t ok = ge_frombytes_w(P, w);
+  if (pos == 0 && j == 0 && meta) meta[key] = (ok ? kKeyDecodes : 0u) | (ge_is_small_order(P) ? kKeySmallOrder : 0u);
+  if (negate) {
+    fe_neg(P.X, P.X);
+    fe_carry(P.X);
+    fe_neg(P.T, P.T);
+    fe_carry(P.T);
+  }
+  ge_niels q;
+  if (ok) comb_entry(q, P, pos, j);
+  else ge_niels_0(q);
+  uint32_t* dst = comb + (((uint64_t)pos * nkeys + key) * kCombEntries + j) * kBStride;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    dst[i] = q.ypx.v[i];
+    dst[10 + i] = q.ymx.v[i];
+    dst[20 + i] = q.xy2d.v[i];
+  }
+  dst[30] = 0;
+  dst[31] = 0;
+}
+
+struct GlobalComb {
+  const uint32_t* comb;
+  uint32_t nkeys, key;
+  NT_D NT_INLINE void load(uint32_t pos, uint32_t idx, ge_niels& q) const {
+    const uint4* e = (const uint4*)(comb + (((uint64_t)pos * nkeys + key) * kCombEntries + idx) * kBStride);
+    uint32_t w[32];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint4 v = e[i];
+      w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      q.ypx.v[i] = w[i];
+      q.ymx.v[i] = w[10 + i];
+      q.xy2d.v[i] = w[20 + i];
+    }
+  }
+};
+
+// Verification against a cached committee: one lane per signature, key_idx[i]
+// selects the key (>= nkeys -> unknown key -> reject).
+template <int MODE>
+__global__ __launch_bounds__(kBlock, 2) void k_ed25519_verify_keyset(
+    const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t n,
+    const uint32_t* __restrict__ meta, const uint32_t* __restrict__ enc, const uint32_t* __restrict__ combA,
+    uint32_t nkeys, const uint32_t* __restrict__ combB, unsigned long long* __restrict__ out_bits) {
+  const uint64_t gi = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t active = gi < n;
+  const uint64_t i = active ? gi : n - 1;
+  const uint32_t kraw = key_idx[i];
+  const uint32_t known = kraw < nkeys;
+  const uint32_t key = known ? kraw : 0u;
+  uint32_t Aw[8], Rw[8], Sw[8];
+  load8(Aw, enc + 8 * key);
+  load8(Rw, sig + 16 * i);
+  load8(Sw, sig + 16 * i + 8);
+  const uint32_t m = known ? meta[key] : 0u;
+  const GlobalComb ca{combA, nkeys, key};
+  const GlobalComb cb{combB, 1u, 0u};
+  const uint32_t ok = active & verify_one_cached<MODE>(m, Aw, Rw, Sw, msg + off[i], len[i], ca, cb);
+  const unsigned long long bal = __ballot(ok);
+  const uint64_t wbase = (uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u);
+  if ((threadIdx.x & 63u) == 0 && wbase < n) out_bits[wbase >> 6] = bal;
+}
+
+// --------------------------------------------------------------------------
 // Certificate groups: AND of the per-signature bits in [first, first + cnt)
 // --------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_group_and(const uint64_t* __restrict__ first,
@@ -309,6 +395,34 @@ hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, const uint64
                      (uint32_t*)d_sig);
   return hipGetLastError();
 }
+
+hipError_t launch_comb_build(const uint32_t* d_enc, uint32_t nkeys, int negate, uint32_t* d_comb,
+                             uint32_t* d_meta, hipStream_t s) {
+  const uint64_t threads = (uint64_t)nkeys * kCombPos * kCombEntries;
+  if (!threads) return hipSuccess;
+  hipLaunchKernelGGL(k_comb_build, dim3((uint32_t)((threads + 127) / 128)), dim3(128), 0, s, d_enc, nkeys, negate,
+                     d_comb, d_meta);
+  return hipGetLastError();
+}
+
+hipError_t launch_verify_keyset(int mode, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
+                                const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
+                                const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
+                                const uint32_t* d_combB, uint64_t* d_out_words, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t blocks = (n + kBlock - 1) / kBlock;
+  if (mode == kStrict)
+    hipLaunchKernelGGL(k_ed25519_verify_keyset<kStrict>, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_key_idx,
+                       (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_meta, d_enc, d_combA, nkeys, d_combB,
+                       (unsigned long long*)d_out_words);
+  else
+    hipLaunchKernelGGL(k_ed25519_verify_keyset<kCofactorless>, dim3((uint32_t)blocks), dim3(kBlock), 0, s,
+                       d_key_idx, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_meta, d_enc, d_combA, nkeys,
+                       d_combB, (unsigned long long*)d_out_words);
+  return hipGetLastError();
+}
+
+size_t comb_bytes_per_key() { return (size_t)kCombPos * kCombEntries * kBStride * 4; }
 
 size_t btab_bytes() { return (size_t)kBEntries * kBStride * 4; }
 size_t ws_bytes_per_slot() { return (size_t)kAEntries * kAQuads * kBlock * 16; }

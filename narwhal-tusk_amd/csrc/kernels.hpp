@@ -18,6 +18,13 @@ hipError_t launch_group_and(const uint64_t* d_first, const uint32_t* d_cnt, uint
 hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, const uint64_t* d_off,
                        const uint64_t* d_len, uint64_t n, const uint32_t* d_btab, uint8_t* d_pk,
                        uint8_t* d_sig, uint32_t max_blocks, hipStream_t s);
+hipError_t launch_comb_build(const uint32_t* d_enc, uint32_t nkeys, int negate, uint32_t* d_comb,
+                             uint32_t* d_meta, hipStream_t s);
+hipError_t launch_verify_keyset(int mode, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
+                                const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
+                                const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
+                                const uint32_t* d_combB, uint64_t* d_out_words, hipStream_t s);
+size_t comb_bytes_per_key();
 size_t btab_bytes();
 size_t ws_bytes_per_slot();
 

@@ -69,6 +69,7 @@ struct Device {
   int ordinal = -1;
   hipStream_t stream = nullptr;
   uint32_t* d_btab = nullptr;
+  uint32_t* d_combB = nullptr;  // comb of B for the key-cache path
   void* d_ws = nullptr;
   uint32_t ws_slots = 0;
   uint32_t sign_blocks = 0;
@@ -86,6 +87,7 @@ struct Device {
     for (auto& b : h)
       if (b.p) (void)hipHostFree(b.p);
     if (d_btab) (void)hipFree(d_btab);
+    if (d_combB) (void)hipFree(d_combB);
     if (d_ws) (void)hipFree(d_ws);
     if (ws_done) (void)hipEventDestroy(ws_done);
     if (stream) (void)hipStreamDestroy(stream);
@@ -101,6 +103,17 @@ struct Device {
     NT_TRY(hipEventCreateWithFlags(&ws_done, hipEventDisableTiming));
     NT_TRY(hipMalloc(&d_btab, nt::btab_bytes()));
     NT_TRY(nt::launch_btab_init(d_btab, stream));
+    {
+      uint32_t* d_benc = nullptr;
+      NT_TRY(hipMalloc(&d_benc, 32));
+      static const uint32_t kB[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                                     0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
+      NT_TRY(hipMemcpyAsync(d_benc, kB, 32, hipMemcpyHostToDevice, stream));
+      NT_TRY(hipMalloc(&d_combB, nt::comb_bytes_per_key()));
+      NT_TRY(nt::launch_comb_build(d_benc, 1, 0, d_combB, nullptr, stream));
+      NT_TRY(hipStreamSynchronize(stream));
+      (void)hipFree(d_benc);
+    }
     // one workspace slot per resident workgroup; default 4 per CU
     uint32_t slots = (uint32_t)prop.multiProcessorCount * 4;
     if (const char* e = std::getenv("NT_WS_SLOTS")) slots = (uint32_t)std::max(1, std::atoi(e));
@@ -128,6 +141,28 @@ struct Device {
 
 struct nt_ctx {
   std::vector<std::unique_ptr<Device>> devs;
+};
+
+struct nt_keyset {
+  nt_ctx* ctx = nullptr;
+  uint32_t nkeys = 0;
+  std::vector<uint32_t> flags;  // host copy of kKey* bits
+  struct PerDev {
+    int ordinal = -1;
+    uint32_t* d_enc = nullptr;
+    uint32_t* d_meta = nullptr;
+    uint32_t* d_comb = nullptr;
+  };
+  std::vector<PerDev> dev;
+  ~nt_keyset() {
+    for (auto& d : dev) {
+      if (d.ordinal < 0) continue;
+      (void)hipSetDevice(d.ordinal);
+      if (d.d_enc) (void)hipFree(d.d_enc);
+      if (d.d_meta) (void)hipFree(d.d_meta);
+      if (d.d_comb) (void)hipFree(d.d_comb);
+    }
+  }
 };
 
 extern "C" {
@@ -452,6 +487,172 @@ int nt_ed25519_keypair_batch(nt_ctx* ctx, const uint8_t* seed32, uint64_t n, uin
   return nt_ed25519_sign_batch(ctx, seed32, nullptr, nullptr, nullptr, n, pk32, nullptr);
 }
 
+// ---- committee key cache --------------------------------------------------
+int nt_keyset_create(nt_ctx* ctx, const uint8_t* pk32, uint32_t nkeys, nt_keyset** out) {
+  if (!ctx || !out || (nkeys && !pk32)) return NT_EINVAL;
+  *out = nullptr;
+  auto ks = std::make_unique<nt_keyset>();
+  ks->ctx = ctx;
+  ks->nkeys = nkeys;
+  ks->flags.assign(nkeys, 0);
+  ks->dev.resize(ctx->devs.size());
+  for (size_t di = 0; di < ctx->devs.size(); ++di) {
+    Device& dv = *ctx->devs[di];
+    std::lock_guard<std::mutex> lk(dv.mu);
+    NT_TRY(hipSetDevice(dv.ordinal));
+    auto& pd = ks->dev[di];
+    pd.ordinal = dv.ordinal;
+    const size_t nk = std::max<uint32_t>(nkeys, 1);
+    if (hipMalloc(&pd.d_enc, 32 * nk) != hipSuccess) return NT_ENOMEM;
+    if (hipMalloc(&pd.d_meta, 4 * nk) != hipSuccess) return NT_ENOMEM;
+    if (hipMalloc(&pd.d_comb, nt::comb_bytes_per_key() * nk) != hipSuccess) return NT_ENOMEM;
+    if (nkeys) {
+      NT_TRY(hipMemcpyAsync(pd.d_enc, pk32, 32ull * nkeys, hipMemcpyHostToDevice, dv.stream));
+      NT_TRY(nt::launch_comb_build(pd.d_enc, nkeys, 1, pd.d_comb, pd.d_meta, dv.stream));
+      if (di == 0)
+        NT_TRY(hipMemcpyAsync(ks->flags.data(), pd.d_meta, 4ull * nkeys, hipMemcpyDeviceToHost, dv.stream));
+    }
+    NT_TRY(hipStreamSynchronize(dv.stream));
+  }
+  *out = ks.release();
+  return NT_OK;
+}
+
+void nt_keyset_free(nt_keyset* ks) { delete ks; }
+
+int nt_keyset_flags(const nt_keyset* ks, uint32_t i, uint32_t* flags) {
+  if (!ks || !flags || i >= ks->nkeys) return NT_EINVAL;
+  *flags = ks->flags[i];
+  return NT_OK;
+}
+
+static int dev_index(nt_ctx* ctx, const Device& dv) {
+  for (size_t i = 0; i < ctx->devs.size(); ++i)
+    if (ctx->devs[i].get() == &dv) return (int)i;
+  return -1;
+}
+
+int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const uint32_t* key_idx,
+                             const uint8_t* sig64, const uint8_t* msg, const uint64_t* off,
+                             const uint64_t* len, uint64_t n, uint8_t* out_bitmap) {
+  if (!ctx || !ks || ks->ctx != ctx || (mode != NT_MODE_STRICT && mode != NT_MODE_COFACTORLESS)) return NT_EINVAL;
+  if (n && (!key_idx || !sig64 || !off || !len || !out_bitmap)) return NT_EINVAL;
+  if (n == 0) return NT_OK;
+  return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
+    const auto& pd = ks->dev[dev_index(ctx, dv)];
+    uint64_t base;
+    NT_CHK(stage_messages(dv, msg, off, len, lo, hi, &base));
+    const uint64_t m = hi - lo, words = (m + 63) / 64;
+    NT_CHK(dv.d[B_PK].ensure(m * 4));
+    NT_CHK(dv.d[B_SIG].ensure(m * 64));
+    NT_CHK(dv.d[B_OUT].ensure(words * 8));
+    NT_CHK(dv.h[B_OUT].ensure(words * 8));
+    NT_TRY(hipMemcpyAsync(dv.d[B_PK].p, key_idx + lo, m * 4, hipMemcpyHostToDevice, dv.stream));
+    NT_TRY(hipMemcpyAsync(dv.d[B_SIG].p, sig64 + 64 * lo, m * 64, hipMemcpyHostToDevice, dv.stream));
+    NT_TRY(nt::launch_verify_keyset(mode, dv.d[B_PK].as<uint32_t>(), dv.d[B_SIG].as<uint8_t>(),
+                                    dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>(),
+                                    dv.d[B_LEN].as<uint64_t>(), m, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys,
+                                    dv.d_combB, dv.d[B_OUT].as<uint64_t>(), dv.stream));
+    NT_TRY(hipMemcpyAsync(dv.h[B_OUT].p, dv.d[B_OUT].p, words * 8, hipMemcpyDeviceToHost, dv.stream));
+    NT_TRY(hipStreamSynchronize(dv.stream));
+    words_to_bitmap(out_bitmap + lo / 8, dv.h[B_OUT].as<uint64_t>(), m);
+    return NT_OK;
+  });
+}
+
+int nt_ed25519_verify_batch_groups_keyset(nt_ctx* ctx, const nt_keyset* ks, const uint32_t* key_idx,
+                                          const uint8_t* sig64, const uint64_t* first,
+                                          const uint32_t* cnt, const uint8_t* msg32, uint64_t G,
+                                          uint8_t* out_group_bitmap, uint8_t* out_sig_bitmap) {
+  if (!ctx || !ks || ks->ctx != ctx) return NT_EINVAL;
+  if (G && (!first || !cnt || !msg32 || !out_group_bitmap)) return NT_EINVAL;
+  if (G == 0) return NT_OK;
+  uint64_t nsig_total = 0;
+  for (uint64_t g = 0; g < G; ++g) nsig_total = std::max(nsig_total, first[g] + cnt[g]);
+  if (nsig_total && (!key_idx || !sig64)) return NT_EINVAL;
+  if (out_sig_bitmap) std::memset(out_sig_bitmap, 0, (nsig_total + 7) / 8);
+  std::mutex sig_mu;
+  return run_sharded(ctx, G, 64, [&](Device& dv, uint64_t glo, uint64_t ghi) -> int {
+    const auto& pd = ks->dev[dev_index(ctx, dv)];
+    const uint64_t gm = ghi - glo;
+    uint64_t m = 0;
+    for (uint64_t g = glo; g < ghi; ++g) m += cnt[g];
+    const uint64_t sw = (m + 63) / 64, gw = (gm + 63) / 64;
+    const uint64_t mm = std::max<uint64_t>(m, 1);
+    NT_CHK(dv.h[B_PK].ensure(mm * 4));
+    NT_CHK(dv.h[B_SIG].ensure(mm * 64));
+    NT_CHK(dv.h[B_OFF].ensure(mm * 8));
+    NT_CHK(dv.h[B_LEN].ensure(mm * 8));
+    NT_CHK(dv.h[B_FIRST].ensure(gm * 8));
+    NT_CHK(dv.h[B_CNT].ensure(gm * 4));
+    NT_CHK(dv.h[B_OUT].ensure(sw * 8 + 8));
+    NT_CHK(dv.h[B_OUT2].ensure(gw * 8));
+    uint32_t* hki = dv.h[B_PK].as<uint32_t>();
+    uint8_t* hsig = dv.h[B_SIG].as<uint8_t>();
+    uint64_t* hoff = dv.h[B_OFF].as<uint64_t>();
+    uint64_t* hlen = dv.h[B_LEN].as<uint64_t>();
+    uint64_t* hfirst = dv.h[B_FIRST].as<uint64_t>();
+    uint32_t* hcnt = dv.h[B_CNT].as<uint32_t>();
+    uint64_t e = 0;
+    for (uint64_t g = glo; g < ghi; ++g) {
+      hfirst[g - glo] = e;
+      hcnt[g - glo] = cnt[g];
+      if (cnt[g]) {
+        std::memcpy(hki + e, key_idx + first[g], 4ull * cnt[g]);
+        std::memcpy(hsig + 64 * e, sig64 + 64 * first[g], 64ull * cnt[g]);
+      }
+      for (uint32_t t = 0; t < cnt[g]; ++t) {
+        hoff[e + t] = 32 * (g - glo);
+        hlen[e + t] = 32;
+      }
+      e += cnt[g];
+    }
+    NT_CHK(dv.d[B_PK].ensure(mm * 4));
+    NT_CHK(dv.d[B_SIG].ensure(mm * 64));
+    NT_CHK(dv.d[B_OFF].ensure(mm * 8));
+    NT_CHK(dv.d[B_LEN].ensure(mm * 8));
+    NT_CHK(dv.d[B_DATA].ensure(gm * 32 + 64));
+    NT_CHK(dv.d[B_FIRST].ensure(gm * 8));
+    NT_CHK(dv.d[B_CNT].ensure(gm * 4));
+    NT_CHK(dv.d[B_OUT].ensure(sw * 8 + 8));
+    NT_CHK(dv.d[B_OUT2].ensure(gw * 8));
+    hipStream_t s = dv.stream;
+    if (m) {
+      NT_TRY(hipMemcpyAsync(dv.d[B_PK].p, hki, m * 4, hipMemcpyHostToDevice, s));
+      NT_TRY(hipMemcpyAsync(dv.d[B_SIG].p, hsig, m * 64, hipMemcpyHostToDevice, s));
+      NT_TRY(hipMemcpyAsync(dv.d[B_OFF].p, hoff, m * 8, hipMemcpyHostToDevice, s));
+      NT_TRY(hipMemcpyAsync(dv.d[B_LEN].p, hlen, m * 8, hipMemcpyHostToDevice, s));
+    }
+    NT_TRY(hipMemcpyAsync(dv.d[B_DATA].p, msg32 + 32 * glo, gm * 32, hipMemcpyHostToDevice, s));
+    NT_TRY(hipMemcpyAsync(dv.d[B_FIRST].p, hfirst, gm * 8, hipMemcpyHostToDevice, s));
+    NT_TRY(hipMemcpyAsync(dv.d[B_CNT].p, hcnt, gm * 4, hipMemcpyHostToDevice, s));
+    NT_TRY(hipMemsetAsync(dv.d[B_OUT].p, 0, sw * 8 + 8, s));
+    NT_TRY(nt::launch_verify_keyset(NT_MODE_COFACTORLESS, dv.d[B_PK].as<uint32_t>(), dv.d[B_SIG].as<uint8_t>(),
+                                    dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>(),
+                                    dv.d[B_LEN].as<uint64_t>(), m, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys,
+                                    dv.d_combB, dv.d[B_OUT].as<uint64_t>(), s));
+    NT_TRY(nt::launch_group_and(dv.d[B_FIRST].as<uint64_t>(), dv.d[B_CNT].as<uint32_t>(), gm,
+                                dv.d[B_OUT].as<uint64_t>(), dv.d[B_OUT2].as<uint64_t>(), s));
+    NT_TRY(hipMemcpyAsync(dv.h[B_OUT2].p, dv.d[B_OUT2].p, gw * 8, hipMemcpyDeviceToHost, s));
+    if (out_sig_bitmap && m)
+      NT_TRY(hipMemcpyAsync(dv.h[B_OUT].p, dv.d[B_OUT].p, sw * 8, hipMemcpyDeviceToHost, s));
+    NT_TRY(hipStreamSynchronize(s));
+    words_to_bitmap(out_group_bitmap + glo / 8, dv.h[B_OUT2].as<uint64_t>(), gm);
+    if (out_sig_bitmap && m) {
+      const uint64_t* bits = dv.h[B_OUT].as<uint64_t>();
+      std::lock_guard<std::mutex> lk(sig_mu);
+      uint64_t e2 = 0;
+      for (uint64_t g = glo; g < ghi; ++g)
+        for (uint32_t t = 0; t < cnt[g]; ++t, ++e2)
+          if ((bits[e2 >> 6] >> (e2 & 63)) & 1) {
+            const uint64_t o = first[g] + t;
+            out_sig_bitmap[o >> 3] |= (uint8_t)(1u << (o & 7));
+          }
+    }
+    return NT_OK;
+  });
+}
+
 // ---- device-resident entry points ---------------------------------------
 int nt_dev_sha512_trunc32(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_data,
                           const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
@@ -485,6 +686,20 @@ int nt_dev_group_and(nt_ctx* ctx, int dev, void* stream, const uint64_t* d_first
   NT_TRY(hipSetDevice(dv->ordinal));
   hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
   NT_TRY(nt::launch_group_and(d_first, d_cnt, G, d_sig_words, d_group_words, s));
+  return NT_OK;
+}
+
+int nt_dev_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int dev, void* stream, int mode,
+                                 const uint32_t* d_key_idx, const uint8_t* d_sig64, const uint8_t* d_msg,
+                                 const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
+                                 uint64_t* d_out_words) {
+  Device* dv = dev_of(ctx, dev);
+  if (!dv || !ks || ks->ctx != ctx || (mode != NT_MODE_STRICT && mode != NT_MODE_COFACTORLESS)) return NT_EINVAL;
+  NT_TRY(hipSetDevice(dv->ordinal));
+  hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
+  const auto& pd = ks->dev[dev];
+  NT_TRY(nt::launch_verify_keyset(mode, d_key_idx, d_sig64, d_msg, d_off, d_len, n, pd.d_meta, pd.d_enc, pd.d_comb,
+                                  ks->nkeys, dv->d_combB, d_out_words, s));
   return NT_OK;
 }
 

@@ -5,13 +5,13 @@ Crate mirror: `Digest, PublicKey, SecretKey, Signature, SignatureService,
 CryptoError, generate_keypair` (crypto/src/lib.rs) and the primary/worker
 callers in `ntcrypto.narwhal` (primary/src/messages.rs, worker/src/processor.rs).
 """
-from ._lib import (EXPORTED, LIB_PATH, NT_MODE_COFACTORLESS, NT_MODE_STRICT, Backend, NtError,
+from ._lib import (EXPORTED, LIB_PATH, NT_MODE_COFACTORLESS, NT_MODE_STRICT, Backend, Keyset, NtError,
                    default_backend, load_library)
 from .crypto import (CryptoError, Digest, PublicKey, SecretKey, Signature, SignatureService,
                      generate_keypair, generate_production_keypair, sha512_digest, sha512_digest_batch)
 
 __all__ = [
-    "Backend", "NtError", "default_backend", "load_library", "EXPORTED", "LIB_PATH",
+    "Backend", "Keyset", "NtError", "default_backend", "load_library", "EXPORTED", "LIB_PATH",
     "NT_MODE_STRICT", "NT_MODE_COFACTORLESS", "CryptoError", "Digest", "PublicKey", "SecretKey",
     "Signature", "SignatureService", "generate_keypair", "generate_production_keypair",
     "sha512_digest", "sha512_digest_batch",

@@ -25,7 +25,9 @@ EXPORTED = [
     "nt_init", "nt_init_device", "nt_free", "nt_num_devices", "nt_strerror", "nt_version",
     "nt_sha512_trunc32", "nt_ed25519_verify_strict", "nt_ed25519_verify_batch_groups",
     "nt_ed25519_sign_batch", "nt_ed25519_keypair_batch", "nt_dev_sha512_trunc32",
-    "nt_dev_ed25519_verify", "nt_dev_group_and", "nt_dev_ed25519_sign",
+    "nt_dev_ed25519_verify", "nt_dev_group_and", "nt_dev_ed25519_sign", "nt_keyset_create",
+    "nt_keyset_free", "nt_keyset_flags", "nt_ed25519_verify_keyset", "nt_ed25519_verify_batch_groups_keyset",
+    "nt_dev_ed25519_verify_keyset",
 ]
 
 
@@ -62,6 +64,15 @@ def load_library(path=None):
                                           _u64, _vp]
     lib.nt_dev_group_and.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _u64, _vp, _vp]
     lib.nt_dev_ed25519_sign.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp]
+    lib.nt_keyset_create.argtypes = [_vp, _u8p, ctypes.c_uint32, ctypes.POINTER(_vp)]
+    lib.nt_keyset_free.argtypes = [_vp]
+    lib.nt_keyset_free.restype = None
+    lib.nt_keyset_flags.argtypes = [_vp, ctypes.c_uint32, _u32p]
+    lib.nt_ed25519_verify_keyset.argtypes = [_vp, _vp, ctypes.c_int, _u32p, _u8p, _u8p, _u64p, _u64p, _u64, _u8p]
+    lib.nt_ed25519_verify_batch_groups_keyset.argtypes = [_vp, _vp, _u32p, _u8p, _u64p, _u32p, _u8p, _u64, _u8p,
+                                                          _u8p]
+    lib.nt_dev_ed25519_verify_keyset.argtypes = [_vp, _vp, ctypes.c_int, _vp, ctypes.c_int, _vp, _vp, _vp, _vp,
+                                                 _vp, _u64, _vp]
     _lib = lib
     return lib
 
@@ -177,6 +188,10 @@ class Backend:
                                               _p(pk), _p(sig)), "nt_ed25519_sign_batch")
         return pk[:n], sig[:n]
 
+    # ---- committee key cache ----
+    def keyset(self, pks):
+        return Keyset(self, pks)
+
     # ---- device-resident (torch tensors or raw pointers) ----
     def dev_verify(self, dev, stream, mode, d_pk, d_sig, d_msg, d_off, d_len, n, d_out):
         _check(self.lib.nt_dev_ed25519_verify(self.ctx, dev, stream, mode, d_pk, d_sig, d_msg, d_off, d_len,
@@ -193,6 +208,73 @@ class Backend:
     def dev_group_and(self, dev, stream, d_first, d_cnt, G, d_sig_words, d_group_words):
         _check(self.lib.nt_dev_group_and(self.ctx, dev, stream, d_first, d_cnt, G, d_sig_words, d_group_words),
                "nt_dev_group_and")
+
+
+class Keyset:
+    """Per-key comb tables of a static committee on every device (nt_keyset_*)."""
+
+    def __init__(self, backend, pks):
+        self.be = backend
+        pks = np.ascontiguousarray(pks, np.uint8).reshape(-1, 32)
+        self.nkeys = len(pks)
+        h = _vp()
+        buf = pks if len(pks) else np.zeros((1, 32), np.uint8)
+        _check(backend.lib.nt_keyset_create(backend.ctx, _p(buf), self.nkeys, ctypes.byref(h)), "nt_keyset_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.be.lib.nt_keyset_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def flags(self, i):
+        f = ctypes.c_uint32()
+        _check(self.be.lib.nt_keyset_flags(self.h, i, ctypes.byref(f)), "nt_keyset_flags")
+        return int(f.value)
+
+    def verify(self, mode, key_idx, sig, msg, off, ln):
+        key_idx = np.ascontiguousarray(key_idx, np.uint32)
+        sig = _u8(sig).reshape(-1, 64)
+        n = len(key_idx)
+        msg = _u8(msg) if len(msg) else np.zeros(1, np.uint8)
+        off = np.ascontiguousarray(off, np.uint64)
+        ln = np.ascontiguousarray(ln, np.uint64)
+        bm = np.zeros((n + 7) // 8 + 1, np.uint8)
+        _check(self.be.lib.nt_ed25519_verify_keyset(self.be.ctx, self.h, mode, _p(key_idx, _u32p), _p(sig), _p(msg),
+                                                    _p(off, _u64p), _p(ln, _u64p), n, _p(bm)),
+               "nt_ed25519_verify_keyset")
+        return _unpack(bm, n)
+
+    def verify_batch_groups(self, key_idx, sig, first, cnt, msg32, with_sig_bits=False):
+        key_idx = np.ascontiguousarray(key_idx, np.uint32)
+        sig = _u8(sig).reshape(-1, 64)
+        if len(key_idx) == 0:
+            key_idx = np.zeros(1, np.uint32)
+            sig = np.zeros((1, 64), np.uint8)
+        first = np.ascontiguousarray(first, np.uint64)
+        cnt = np.ascontiguousarray(cnt, np.uint32)
+        msg32 = _u8(msg32).reshape(-1, 32)
+        G = len(cnt)
+        nsig = int((first + cnt).max()) if G else 0
+        gb = np.zeros((G + 7) // 8 + 1, np.uint8)
+        sb = np.zeros((nsig + 7) // 8 + 1, np.uint8)
+        _check(self.be.lib.nt_ed25519_verify_batch_groups_keyset(
+            self.be.ctx, self.h, _p(key_idx, _u32p), _p(sig), _p(first, _u64p), _p(cnt, _u32p), _p(msg32), G,
+            _p(gb), _p(sb) if with_sig_bits else None), "nt_ed25519_verify_batch_groups_keyset")
+        if with_sig_bits:
+            return _unpack(gb, G), _unpack(sb, nsig)
+        return _unpack(gb, G)
+
+    def dev_verify(self, dev, stream, mode, d_key_idx, d_sig, d_msg, d_off, d_len, n, d_out):
+        _check(self.be.lib.nt_dev_ed25519_verify_keyset(self.be.ctx, self.h, dev, stream, mode, d_key_idx, d_sig,
+                                                        d_msg, d_off, d_len, n, d_out),
+               "nt_dev_ed25519_verify_keyset")
 
 
 _default = None

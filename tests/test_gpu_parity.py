@@ -190,3 +190,56 @@ def test_batch_corpus_rule(be, corpus):
     msg32 = np.stack([corpus["msg"][int(corpus["off"][i]):int(corpus["off"][i]) + 32] for i in sel])
     gb = be.verify_batch_groups(pk, sig, np.arange(len(sel), dtype=np.uint64), np.ones(len(sel), np.uint32), msg32)
     assert np.array_equal(gb, corpus["batch_rule"][sel].astype(bool))
+
+
+# ------------------------------------------------------------------ committee key cache
+def test_keyset_corpus(be, corpus):
+    """Every corpus key (incl. off-curve, small-order, non-canonical) as a keyset entry."""
+    ks = be.keyset(corpus["pk"])
+    n = len(corpus["pk"])
+    idx = np.arange(n, dtype=np.uint32)
+    import ntcrypto
+    got_s = ks.verify(ntcrypto.NT_MODE_STRICT, idx, corpus["sig"], corpus["msg"], corpus["off"], corpus["len"])
+    assert np.array_equal(got_s, corpus["strict"].astype(bool))
+    got_c = ks.verify(ntcrypto.NT_MODE_COFACTORLESS, idx, corpus["sig"], corpus["msg"], corpus["off"], corpus["len"])
+    assert np.array_equal(got_c, corpus["batch_rule"].astype(bool))
+    # unknown key index -> reject
+    bad = ks.verify(ntcrypto.NT_MODE_STRICT, np.full(n, n + 5, np.uint32), corpus["sig"], corpus["msg"],
+                    corpus["off"], corpus["len"])
+    assert not bad.any()
+    ks.close()
+
+
+def test_keyset_batch_groups_fixture(be):
+    g = np.load(os.path.join(GOLD, "batch_groups.npz"))
+    uniq, inv = np.unique(g["pk"], axis=0, return_inverse=True)
+    ks = be.keyset(uniq)
+    gb, sb = ks.verify_batch_groups(inv.astype(np.uint32).ravel(), g["sig"], g["first"], g["cnt"], g["msg32"],
+                                    with_sig_bits=True)
+    assert np.array_equal(gb, g["expect"].astype(bool))
+    gb2, sb2 = be.verify_batch_groups(g["pk"], g["sig"], g["first"], g["cnt"], g["msg32"], with_sig_bits=True)
+    assert np.array_equal(sb, sb2)
+    ks.close()
+
+
+def test_keyset_committee_random_vs_oracle(be, oracle):
+    rng = np.random.default_rng(3)
+    nk, n = 100, 5000
+    seeds = rng.integers(0, 256, (nk, 32), dtype=np.uint8)
+    pks = be.sign_batch(seeds)
+    ks = be.keyset(pks)
+    key_idx = rng.integers(0, nk, n).astype(np.uint32)
+    msgs = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in rng.integers(0, 300, n)]
+    data, off, ln = _pack(msgs)
+    _, sig = be.sign_batch(seeds[key_idx], data, off, ln)
+    sig = sig.copy()
+    flip = rng.random(n) < 0.3
+    sig[flip, 7] ^= 0x10
+    import ntcrypto
+    got = ks.verify(ntcrypto.NT_MODE_STRICT, key_idx, sig, data, off, ln)
+    want = oracle.verify_strict_many(pks[key_idx], sig, data, off, ln, nthreads=8).astype(bool)
+    assert np.array_equal(got, want)
+    assert got.sum() == (~flip).sum()
+    flags = [ks.flags(i) for i in range(nk)]
+    assert all(f == 1 for f in flags)
+    ks.close()
