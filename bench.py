@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--sha-msgs", type=int, default=16384, help="config 4 messages (total, sharded)")
     ap.add_argument("--sha-len", type=int, default=500_000)
     ap.add_argument("--no-sha", action="store_true")
+    ap.add_argument("--certs", type=int, default=100_000, help="config 3 certificates (total, sharded)")
+    ap.add_argument("--committee", type=int, default=100)
+    ap.add_argument("--no-certs", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-seconds of baseline work")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -192,6 +195,10 @@ def main():
     if not args.no_sha:
         line["sha512"] = bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_ranks)
 
+    # ---------------------------------------------------------------- config 3: certificates
+    if not args.no_certs:
+        line["certificates"] = bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_ranks)
+
     # ---------------------------------------------------------------- CPU baseline (rank 0, N=1)
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args, pk_h, sig_h, msg_h, L, got)
@@ -245,6 +252,137 @@ def bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_r
             "hbm_frac": round((m * padded / (kms * 1e-3)) / 1e9 / HBM_PEAK_GBS, 4),
             "note": "one lane per message: 16,384 lanes = 256 waves, latency-bound (SURVEY H2)",
             "spot_check_ok": bool(ok)}
+
+
+def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_ranks):
+    """Config 3: Certificate::verify (primary/src/messages.rs:189-215) for 100k
+    certificates of an n=100 committee, 2f+1 = 67 votes each, sharded over ranks.
+    Per certificate on the GPU: SHA-512 of the header preimage (id check,
+    messages.rs:70-84), SHA-512 of the certificate digest preimage (:226-234),
+    verify_strict of the header signature, cofactorless verify of the 67 votes,
+    group AND -- against the committee key cache (nt_keyset) and, for
+    comparison, through the uncached verify path."""
+    import hashlib
+    import struct
+    import ntcrypto
+
+    nk = args.committee
+    quorum = 2 * nk // 3 + 1                      # config/src/lib.rs:168-173 with stake 1
+    G_total = args.certs
+    G = (G_total + world - 1) // world
+    G = max(0, min(G, G_total - rank * G))
+    n_pay, n_par = 32, quorum                      # header_size 1,000 B / 32 B digests; 2f+1 parents
+    hlen = 32 + 8 + 36 * n_pay + 32 * n_par
+    seeds_h = np.stack([np.frombuffer(hashlib.sha512(b"nt-bench-key" + struct.pack("<Q", i)).digest()[:32], np.uint8)
+                        for i in range(nk)])
+    seeds = torch.from_numpy(seeds_h).to(dev)
+    pks = be.sign_batch(seeds_h)
+    ks = be.keyset(pks)
+    pks_d = torch.from_numpy(pks).to(dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(777 + rank)
+    author = torch.randint(0, nk, (G,), device=dev, generator=g)
+    rnd = torch.randint(1, 1 << 20, (G,), device=dev, generator=g, dtype=torch.int64)
+    hdr = torch.randint(0, 256, (G, hlen), dtype=torch.uint8, device=dev, generator=g)
+    hdr[:, 0:32] = pks_d[author]
+    hdr[:, 32:40] = rnd.view(-1, 1).bitwise_right_shift(torch.arange(0, 64, 8, device=dev)).bitwise_and(255).to(torch.uint8)
+    wid = 40 + 36 * torch.arange(n_pay, device=dev).view(-1, 1) + 32 + torch.arange(4, device=dev).view(1, -1)
+    hdr[:, wid.reshape(-1)] = 0                    # worker id 0
+    hdr_flat = hdr.reshape(-1).contiguous()
+    h_off = torch.arange(G, dtype=torch.int64, device=dev) * hlen
+    h_len = torch.full((G,), hlen, dtype=torch.int64, device=dev)
+    ids = torch.empty((G, 32), dtype=torch.uint8, device=dev)
+    be.dev_sha512(0, sp, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, ids.data_ptr())
+    # header signatures by the author over the id
+    i_off = torch.arange(G, dtype=torch.int64, device=dev) * 32
+    i_len = torch.full((G,), 32, dtype=torch.int64, device=dev)
+    hsig = torch.empty((G, 64), dtype=torch.uint8, device=dev)
+    tmp_pk = torch.empty((G, 32), dtype=torch.uint8, device=dev)
+    be.dev_sign(0, sp, seeds[author].contiguous().data_ptr(), ids.data_ptr(), i_off.data_ptr(), i_len.data_ptr(), G,
+                tmp_pk.data_ptr(), hsig.data_ptr())
+    # certificate digest preimage: id || round_le || origin
+    cpre = torch.cat([ids, hdr[:, 32:40], hdr[:, 0:32]], dim=1).contiguous()
+    c_off = torch.arange(G, dtype=torch.int64, device=dev) * 72
+    c_len = torch.full((G,), 72, dtype=torch.int64, device=dev)
+    cdig = torch.empty((G, 32), dtype=torch.uint8, device=dev)
+    be.dev_sha512(0, sp, cpre.data_ptr(), c_off.data_ptr(), c_len.data_ptr(), G, cdig.data_ptr())
+    # 67 distinct voters per certificate, signatures over the certificate digest
+    voters = torch.rand((G, nk), device=dev, generator=g).argsort(dim=1)[:, :quorum].contiguous()
+    V = G * quorum
+    vkey = voters.reshape(-1).to(torch.int32).contiguous()
+    v_off = (torch.arange(V, device=dev, dtype=torch.int64) // quorum) * 32
+    v_len = torch.full((V,), 32, dtype=torch.int64, device=dev)
+    vsig = torch.empty((V, 64), dtype=torch.uint8, device=dev)
+    vpk = torch.empty((V, 32), dtype=torch.uint8, device=dev)
+    be.dev_sign(0, sp, seeds[voters.reshape(-1)].contiguous().data_ptr(), cdig.data_ptr(), v_off.data_ptr(),
+                v_len.data_ptr(), V, vpk.data_ptr(), vsig.data_ptr())
+    # 1 % of certificates carry one corrupted vote
+    rng = np.random.default_rng(99 + rank)
+    bad = np.sort(rng.choice(G, size=max(1, G // 100), replace=False)) if G else np.zeros(0, np.int64)
+    if len(bad):
+        rows = torch.from_numpy(bad * quorum + rng.integers(0, quorum, len(bad))).to(dev)
+        vsig[rows, 40] ^= 0x01
+    expect = np.ones(G, dtype=bool)
+    expect[bad] = False
+    torch.cuda.synchronize(dev)
+
+    first = torch.arange(G, dtype=torch.int64, device=dev) * quorum
+    cnt = torch.full((G,), quorum, dtype=torch.int32, device=dev)
+    hkey = author.to(torch.int32).contiguous()
+    hd2 = torch.empty((G, 32), dtype=torch.uint8, device=dev)
+    cd2 = torch.empty((G, 32), dtype=torch.uint8, device=dev)
+    hbits = torch.zeros(((G + 63) // 64,), dtype=torch.int64, device=dev)
+    vbits = torch.zeros(((V + 63) // 64 + 1,), dtype=torch.int64, device=dev)
+    gbits = torch.zeros(((G + 63) // 64,), dtype=torch.int64, device=dev)
+
+    def step(cached):
+        be.dev_sha512(0, sp, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, hd2.data_ptr())
+        be.dev_sha512(0, sp, cpre.data_ptr(), c_off.data_ptr(), c_len.data_ptr(), G, cd2.data_ptr())
+        if cached:
+            ks.dev_verify(0, sp, ntcrypto.NT_MODE_STRICT, hkey.data_ptr(), hsig.data_ptr(), ids.data_ptr(),
+                          i_off.data_ptr(), i_len.data_ptr(), G, hbits.data_ptr())
+            ks.dev_verify(0, sp, ntcrypto.NT_MODE_COFACTORLESS, vkey.data_ptr(), vsig.data_ptr(), cd2.data_ptr(),
+                          v_off.data_ptr(), v_len.data_ptr(), V, vbits.data_ptr())
+        else:
+            be.dev_verify(0, sp, ntcrypto.NT_MODE_STRICT, tmp_pk.data_ptr(), hsig.data_ptr(), ids.data_ptr(),
+                          i_off.data_ptr(), i_len.data_ptr(), G, hbits.data_ptr())
+            be.dev_verify(0, sp, ntcrypto.NT_MODE_COFACTORLESS, vpk.data_ptr(), vsig.data_ptr(), cd2.data_ptr(),
+                          v_off.data_ptr(), v_len.data_ptr(), V, vbits.data_ptr())
+        be.dev_group_and(0, sp, first.data_ptr(), cnt.data_ptr(), G, vbits.data_ptr(), gbits.data_ptr())
+
+    def verdicts():
+        gb = np.unpackbits(gbits.cpu().numpy().view(np.uint8), bitorder="little")[:G].astype(bool)
+        hb = np.unpackbits(hbits.cpu().numpy().view(np.uint8), bitorder="little")[:G].astype(bool)
+        idok = (hd2 == ids).all(dim=1).cpu().numpy()
+        return gb & hb & idok
+
+    out = {}
+    steps = max(1, min(args.steps, 5))
+    for cached in (True, False):
+        for _ in range(max(1, args.warmup)):
+            step(cached)
+        barrier()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(steps):
+            step(cached)
+        ev1.record(stream)
+        barrier()
+        wall = max_over_ranks(time.perf_counter() - t0)
+        kms = ev0.elapsed_time(ev1) / steps
+        mism = int(max_over_ranks(int((verdicts() != expect).sum())))
+        key = "keyset" if cached else "uncached"
+        out[key] = {"certs_per_s": round(G_total * steps / wall, 1),
+                    "sig_verifies_per_s": round(G_total * (quorum + 1) * steps / wall, 1),
+                    "ms_per_step": round(wall * 1e3 / steps, 3), "gpu_ms_per_step": round(kms, 3),
+                    "mismatches_vs_expected": mism}
+    ks.close()
+    return {"value": out["keyset"]["certs_per_s"], "unit": "certificates/s",
+            "workload": "cfg3: %d certificates, committee n=%d, %d votes + 1 header signature each, "
+                        "%d-byte header preimage" % (G_total, nk, quorum, hlen),
+            "scaling": "strong (certificates sharded over ranks)", **out}
 
 
 def cpu_baseline(args, pk_h, sig_h, msg_h, L, got):
