@@ -89,12 +89,10 @@ def main():
         if world > 1:
             dist.barrier()
 
+    from ntcrypto import dist as nd
+
     def max_over_ranks(x):
-        if world == 1:
-            return x
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        return nd.reduce_max(x)
 
     # ---------------------------------------------------------------- inputs (config 2)
     n, L = args.n, args.msg_len
@@ -211,9 +209,10 @@ def main():
 
 
 def bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_ranks):
+    from ntcrypto import dist as nd
     m_total, ml = args.sha_msgs, args.sha_len
-    m = (m_total + world - 1) // world  # this rank's shard of the 16,384 messages
-    m = min(m, m_total - rank * m) if rank * m < m_total else 0
+    lo, hi = nd.shard(m_total, world, rank)  # this rank's shard of the 16,384 messages
+    m = hi - lo
     g = torch.Generator(device=dev)
     g.manual_seed(4242 + rank)
     data = torch.randint(0, 256, (m * ml + 64,), dtype=torch.uint8, device=dev, generator=g)
@@ -268,9 +267,10 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
 
     nk = args.committee
     quorum = 2 * nk // 3 + 1                      # config/src/lib.rs:168-173 with stake 1
+    from ntcrypto import dist as nd
     G_total = args.certs
-    G = (G_total + world - 1) // world
-    G = max(0, min(G, G_total - rank * G))
+    glo, ghi = nd.shard(G_total, world, rank)
+    G = ghi - glo
     n_pay, n_par = 32, quorum                      # header_size 1,000 B / 32 B digests; 2f+1 parents
     hlen = 32 + 8 + 36 * n_pay + 32 * n_par
     seeds_h = np.stack([np.frombuffer(hashlib.sha512(b"nt-bench-key" + struct.pack("<Q", i)).digest()[:32], np.uint8)

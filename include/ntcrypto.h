@@ -62,6 +62,10 @@ typedef struct nt_ctx nt_ctx;
 int nt_init(nt_ctx **out, int num_gpus);
 /* One specific device ordinal (used by one-process-per-GPU launchers). */
 int nt_init_device(nt_ctx **out, int device_ordinal);
+/* An explicit list of device ordinals; repeats are allowed (each entry gets
+ * its own stream, tables and workspace), which lets the multi-device sharding
+ * of the host entry points be exercised on a single GPU. */
+int nt_init_devices(nt_ctx **out, const int *ordinals, int n);
 void nt_free(nt_ctx *ctx);
 int nt_num_devices(const nt_ctx *ctx);
 const char *nt_strerror(int code);

@@ -212,6 +212,16 @@ int nt_init_device(nt_ctx** out, int device_ordinal) {
   return init_common(out, {device_ordinal});
 }
 
+int nt_init_devices(nt_ctx** out, const int* ordinals, int n) {
+  int count = 0;
+  if (!ordinals || n <= 0) return NT_EINVAL;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return NT_ENODEV;
+  std::vector<int> ords(ordinals, ordinals + n);
+  for (int o : ords)
+    if (o < 0 || o >= count) return NT_EINVAL;
+  return init_common(out, ords);
+}
+
 void nt_free(nt_ctx* ctx) { delete ctx; }
 
 int nt_num_devices(const nt_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }

@@ -22,7 +22,7 @@ _vp = ctypes.c_void_p
 _u64 = ctypes.c_uint64
 
 EXPORTED = [
-    "nt_init", "nt_init_device", "nt_free", "nt_num_devices", "nt_strerror", "nt_version",
+    "nt_init", "nt_init_device", "nt_init_devices", "nt_free", "nt_num_devices", "nt_strerror", "nt_version",
     "nt_sha512_trunc32", "nt_ed25519_verify_strict", "nt_ed25519_verify_batch_groups",
     "nt_ed25519_sign_batch", "nt_ed25519_keypair_batch", "nt_dev_sha512_trunc32",
     "nt_dev_ed25519_verify", "nt_dev_group_and", "nt_dev_ed25519_sign", "nt_keyset_create",
@@ -49,6 +49,7 @@ def load_library(path=None):
     lib = ctypes.CDLL(p)
     lib.nt_init.argtypes = [ctypes.POINTER(_vp), ctypes.c_int]
     lib.nt_init_device.argtypes = [ctypes.POINTER(_vp), ctypes.c_int]
+    lib.nt_init_devices.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     lib.nt_free.argtypes = [_vp]
     lib.nt_free.restype = None
     lib.nt_num_devices.argtypes = [_vp]
@@ -98,10 +99,13 @@ def _unpack(bm, n):
 class Backend:
     """A context over one or more gfx950 devices (nt_init / nt_init_device)."""
 
-    def __init__(self, num_gpus=0, device=None):
+    def __init__(self, num_gpus=0, device=None, devices=None):
         self.lib = load_library()
         ctx = _vp()
-        if device is not None:
+        if devices is not None:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            rc = self.lib.nt_init_devices(ctypes.byref(ctx), arr, len(devices))
+        elif device is not None:
             rc = self.lib.nt_init_device(ctypes.byref(ctx), int(device))
         else:
             rc = self.lib.nt_init(ctypes.byref(ctx), int(num_gpus))

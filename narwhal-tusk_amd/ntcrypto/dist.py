@@ -1,0 +1,51 @@
+"""Host-side multi-GPU plumbing: the path shards by index and has
+no exchange step, so ranks only need (1) their contiguous shard and (2) a
+barrier + max-over-ranks wall time for reporting.  torch.distributed with the
+gloo backend is used for that control plane only -- no RCCL on the data path.
+"""
+import os
+
+
+def world_info():
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def shard(total: int, world: int, rank: int, align: int = 1):
+    """Contiguous [lo, hi) of `total` items for `rank`; boundaries are multiples
+    of `align` (64 keeps verdict bitmap words whole) except the final end."""
+    per = -(-total // world) if world else total
+    per = -(-per // align) * align
+    lo = min(total, rank * per)
+    hi = min(total, lo + per)
+    return lo, hi
+
+
+def reduce_max(x: float) -> float:
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return x
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def reduce_sum(x: float) -> float:
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return x
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def gather_bytes(local: bytes, world: int):
+    """All ranks' byte strings (verdict bitmaps / digests) on every rank."""
+    import torch.distributed as dist
+    if world == 1:
+        return [local]
+    out = [None] * world
+    dist.all_gather_object(out, local)
+    return out
