@@ -72,6 +72,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
+    # NT_BENCH_DEVICE pins every rank to one ordinal (rehearsing N>1 on a 1-GPU box)
+    local = int(os.environ.get("NT_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

@@ -7,7 +7,7 @@ set -euo pipefail
 OUT=${1:-gpurun_out/pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="python3 bench.py --steps 1 --warmup 0 --no-cpu"
+BENCH="python3 bench.py --steps 1 --warmup 0 --no-cpu ${PMC_BENCH_ARGS:-}"
 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" \

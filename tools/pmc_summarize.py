@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Summarize tools/pmc_collect.sh output into a per-launch JSON for profiles/.
+
+Per kernel: counters summed over its dispatches and divided by the dispatch
+count (per launch).  HBM traffic per launch = FETCH_SIZE*1024*2 (gfx950 reports
+half the bytes of wide 16-B/lane streaming reads; MI355X_MICROARCH.md §HBM) +
+WRITE_SIZE*1024; the uncorrected read figure is kept beside it.
+VALU issue share = SQ_INSTS_VALU * 4 cycles / (SIMDs * GRBM_GUI_ACTIVE/8).
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+KERNELS = {"k_ed25519_verify_keyset": "verify_keyset", "k_ed25519_verify<": "verify", "k_sha512": "sha512",
+           "k_ed25519_sign": "sign", "k_group_and": "group_and"}
+
+
+def kname(k):
+    for pat, name in KERNELS.items():
+        if pat in k:
+            return name
+    return None
+
+
+def main(indir, out, tag):
+    acc = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(lambda: collections.defaultdict(set))
+    for f in sorted(glob.glob(os.path.join(indir, "pass*", "*counter_collection.csv"))):
+        pdir = os.path.basename(os.path.dirname(f))
+        for r in csv.DictReader(open(f)):
+            n = kname(r["Kernel_Name"])
+            if not n:
+                continue
+            acc[n][r["Counter_Name"]] += float(r["Counter_Value"])
+            disp[n][pdir].add(r["Dispatch_Id"])
+    res = {"tag": tag, "source": indir, "kernels": {}}
+    for n, c in acc.items():
+        nd = max(len(v) for v in disp[n].values())
+        per = {k: v / nd for k, v in c.items()}
+        d = {"dispatches_per_pass": nd, "per_launch": per}
+        if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
+            d["hbm_bytes_per_launch"] = per["FETCH_SIZE"] * 1024 * 2 + per["WRITE_SIZE"] * 1024
+            d["hbm_bytes_per_launch_uncorrected"] = (per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024
+        if "SQ_INSTS_VALU" in per and "GRBM_GUI_ACTIVE" in per:
+            cyc = per["GRBM_GUI_ACTIVE"] / 8
+            d["valu_issue_share_4cyc"] = per["SQ_INSTS_VALU"] * 4 / (1024 * cyc)
+        res["kernels"][n] = d
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1)[:3000])
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "")
