@@ -334,3 +334,111 @@ NT_HD NT_INLINE uint32_t verify_one_cached(uint32_t meta, const uint32_t Aw[8], 
 }
 
 }  // namespace nt
+
+namespace nt {
+
+// ---------------------------------------------------------------------------
+// Cached verification of TWO signatures per lane with one shared inversion.
+//
+// R is never decompressed.  For R' = [s]B - [k]A with affine (x', y'):
+//   dalek accepts  <=>  R decodes to a point equal to R'
+//                  <=>  y_R == y' (mod p)  and  (sign(R) == parity(x')  or  x' == 0)
+// (R's y is taken mod p exactly as curve25519-dalek's from_bytes does; a valid
+// R' makes R decodable whenever y matches; x' = 0 covers the accepted
+// "negative zero" encodings).  In strict mode the small-order test of R is done
+// on R' (equal points have equal order; if they differ the verdict is reject
+// anyway).  The two Z^-1 come from one exponentiation (Montgomery's trick).
+// ---------------------------------------------------------------------------
+template <class CombA, class CombB>
+NT_HD NT_INLINE void comb_ladder(ge_p3& acc, const uint32_t k[8], const uint32_t Sw[8], const CombA& ca,
+                                 const CombB& cb) {
+  uint32_t kd[8], sd[8];
+  sc_recode_w8(kd, k);
+  sc_recode_w8(sd, Sw);
+  ge_p3_0(acc);
+  ge_cp t;
+#pragma unroll 1
+  for (int w = 0; w < 8; ++w) {
+    const uint32_t kw = kd[0], sw = sd[0];
+#pragma unroll
+    for (int m = 0; m < 7; ++m) { kd[m] = kd[m + 1]; sd[m] = sd[m + 1]; }
+#pragma unroll 1
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t pos = 4 * w + b;
+      const int32_t dk = (int32_t)(((kw >> (8 * b)) & 255u) ^ 128u) - 128;
+      const int32_t ds = (int32_t)(((sw >> (8 * b)) & 255u) ^ 128u) - 128;
+      ge_niels ne;
+      ca.load(pos, (uint32_t)(dk < 0 ? -dk : dk), ne);
+      ge_niels_cneg(ne, dk < 0);
+      ge_add_niels(t, acc, ne);
+      ge_cp_to_p3(acc, t);
+      cb.load(pos, (uint32_t)(ds < 0 ? -ds : ds), ne);
+      ge_niels_cneg(ne, ds < 0);
+      ge_add_niels(t, acc, ne);
+      ge_cp_to_p3(acc, t);
+    }
+  }
+}
+
+NT_HD NT_INLINE void hram_scalar(uint32_t k[8], const uint32_t Rw[8], const uint32_t Aw[8], const uint8_t* msg,
+                                 uint64_t len) {
+  uint32_t prefix[16];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) { prefix[q] = Rw[q]; prefix[8 + q] = Aw[q]; }
+  uint64_t st[8];
+  sha512_prefixed<16>(st, prefix, msg, len);
+  uint32_t hw[16];
+  sha512_out_words(hw, st, 16);
+  sc_reduce512(k, hw);
+}
+
+// compare affine (x, y) with the encoding Rw under dalek decode semantics
+NT_HD NT_INLINE uint32_t enc_matches(const fe& x, const fe& y, const uint32_t Rw[8]) {
+  fe yr;
+  fe_frombytes_w(yr, Rw);  // bit 255 dropped, value taken mod p by the compare
+  uint32_t a[8], b[8], xw[8];
+  fe_tobytes_w(a, y);
+  fe_tobytes_w(b, yr);
+  fe_tobytes_w(xw, x);
+  uint32_t same = 1, xz = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    same &= (a[i] == b[i]);
+    xz |= xw[i];
+  }
+  const uint32_t sign = Rw[7] >> 31;
+  return same & (((xw[0] & 1u) == sign) | (xz == 0));
+}
+
+template <int MODE, class CombA, class CombB>
+NT_HD NT_INLINE void verify_two_cached(uint32_t ok[2], const uint32_t meta[2], const uint32_t Aw[2][8],
+                                       const uint32_t Rw[2][8], const uint32_t Sw[2][8], const uint8_t* msg[2],
+                                       const uint64_t len[2], const CombA ca[2], const CombB& cb) {
+  ge_p2 P[2];
+#pragma unroll 1
+  for (int j = 0; j < 2; ++j) {
+    ok[j] = sc_is_canonical(Sw[j]) & (meta[j] & kKeyDecodes ? 1u : 0u);
+    if (MODE == kStrict) ok[j] &= (meta[j] & kKeySmallOrder) ? 0u : 1u;
+    uint32_t k[8];
+    hram_scalar(k, Rw[j], Aw[j], msg[j], len[j]);
+    ge_p3 acc;
+    comb_ladder(acc, k, Sw[j], ca[j], cb);
+    ge_p3_to_p2(P[j], acc);
+  }
+  // Z0^-1, Z1^-1 from one inversion
+  fe zz, inv, zi0, zi1;
+  fe_mul(zz, P[0].Z, P[1].Z);
+  fe_invert(inv, zz);
+  fe_mul(zi0, inv, P[1].Z);
+  fe_mul(zi1, inv, P[0].Z);
+#pragma unroll 1
+  for (int j = 0; j < 2; ++j) {
+    fe x, y;
+    fe_mul(x, P[j].X, j ? zi1 : zi0);
+    fe_mul(y, P[j].Y, j ? zi1 : zi0);
+    ok[j] &= enc_matches(x, y, Rw[j]);
+    if (MODE == kStrict) ok[j] &= ge_is_small_order_p2(P[j]) ^ 1u;
+  }
+}
+
+}  // namespace nt

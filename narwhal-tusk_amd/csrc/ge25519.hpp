@@ -199,12 +199,16 @@ NT_HD NT_INLINE uint32_t ge_p2_is_identity(const ge_p2& p) {
 }
 
 // [8]P == identity  (EdwardsPoint::is_small_order)
-NT_HD NT_INLINE uint32_t ge_is_small_order(const ge_p3& p) {
-  ge_p2 t;
-  ge_p3_to_p2(t, p);
+NT_HD NT_INLINE uint32_t ge_is_small_order_p2(const ge_p2& p) {
+  ge_p2 t = p;
 #pragma unroll 1
   for (int i = 0; i < 3; ++i) ge_dbl_p2(t, t);
   return ge_p2_is_identity(t);
+}
+NT_HD NT_INLINE uint32_t ge_is_small_order(const ge_p3& p) {
+  ge_p2 t;
+  ge_p3_to_p2(t, p);
+  return ge_is_small_order_p2(t);
 }
 
 // Projective equality of a p2 point with a p3 point whose Z = 1 (decompressed).

@@ -226,31 +226,46 @@ struct GlobalComb {
   }
 };
 
-// Verification against a cached committee: one lane per signature, key_idx[i]
-// selects the key (>= nkeys -> unknown key -> reject).
+// Verification against a cached committee: each lane verifies TWO signatures
+// (wave w, lane l: signatures 128w + l and 128w + 64 + l) sharing one field
+// inversion; key_idx[i] selects the key (>= nkeys -> unknown key -> reject).
 template <int MODE>
 __global__ __launch_bounds__(kBlock, 2) void k_ed25519_verify_keyset(
     const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t n,
     const uint32_t* __restrict__ meta, const uint32_t* __restrict__ enc, const uint32_t* __restrict__ combA,
     uint32_t nkeys, const uint32_t* __restrict__ combB, unsigned long long* __restrict__ out_bits) {
-  const uint64_t gi = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t active = gi < n;
-  const uint64_t i = active ? gi : n - 1;
-  const uint32_t kraw = key_idx[i];
-  const uint32_t known = kraw < nkeys;
-  const uint32_t key = known ? kraw : 0u;
-  uint32_t Aw[8], Rw[8], Sw[8];
-  load8(Aw, enc + 8 * key);
-  load8(Rw, sig + 16 * i);
-  load8(Sw, sig + 16 * i + 8);
-  const uint32_t m = known ? meta[key] : 0u;
-  const GlobalComb ca{combA, nkeys, key};
+  const uint64_t wave = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t act[2], m[2], Aw[2][8], Rw[2][8], Sw[2][8];
+  const uint8_t* mp[2];
+  uint64_t ml[2];
+  GlobalComb ca[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const uint64_t gi = 128 * wave + 64 * j + lane;
+    act[j] = gi < n;
+    const uint64_t i = act[j] ? gi : n - 1;
+    const uint32_t kraw = key_idx[i];
+    const uint32_t known = kraw < nkeys;
+    const uint32_t key = known ? kraw : 0u;
+    load8(Aw[j], enc + 8 * key);
+    load8(Rw[j], sig + 16 * i);
+    load8(Sw[j], sig + 16 * i + 8);
+    m[j] = known ? meta[key] : 0u;
+    mp[j] = msg + off[i];
+    ml[j] = len[i];
+    ca[j] = GlobalComb{combA, nkeys, key};
+  }
   const GlobalComb cb{combB, 1u, 0u};
-  const uint32_t ok = active & verify_one_cached<MODE>(m, Aw, Rw, Sw, msg + off[i], len[i], ca, cb);
-  const unsigned long long bal = __ballot(ok);
-  const uint64_t wbase = (uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u);
-  if ((threadIdx.x & 63u) == 0 && wbase < n) out_bits[wbase >> 6] = bal;
+  uint32_t ok[2];
+  verify_two_cached<MODE>(ok, m, Aw, Rw, Sw, mp, ml, ca, cb);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const unsigned long long bal = __ballot(ok[j] & act[j]);
+    const uint64_t wbase = 128 * wave + 64 * j;
+    if (lane == 0 && wbase < n) out_bits[wbase >> 6] = bal;
+  }
 }
 
 // --------------------------------------------------------------------------
@@ -410,7 +425,7 @@ hipError_t launch_verify_keyset(int mode, const uint32_t* d_key_idx, const uint8
                                 const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
                                 const uint32_t* d_combB, uint64_t* d_out_words, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const uint64_t blocks = (n + kBlock - 1) / kBlock;
+  const uint64_t blocks = (n + 2 * kBlock - 1) / (2 * kBlock);  // two signatures per lane
   if (mode == kStrict)
     hipLaunchKernelGGL(k_ed25519_verify_keyset<kStrict>, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_key_idx,
                        (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_meta, d_enc, d_combA, nkeys, d_combB,
