@@ -1,6 +1,8 @@
 // crypto.cpp -- implementation of the crypto crate mirror over include/ntcrypto.h.
 #include "crypto.hpp"
 
+#include <algorithm>
+#include <climits>
 #include <cstring>
 #include <random>
 
@@ -224,6 +226,82 @@ std::vector<bool> verify_batch_many(
 
 void Signature::verify_batch(const Digest& digest, const std::vector<std::pair<PublicKey, Signature>>& votes) {
   if (!verify_batch_many({digest}, {&votes})[0]) throw CryptoError();
+}
+
+KeySet::KeySet(const std::vector<PublicKey>& keys) : keys_(keys) {
+  std::vector<uint8_t> pk(32 * std::max<size_t>(keys.size(), 1));
+  for (size_t i = 0; i < keys.size(); ++i) {
+    std::memcpy(&pk[32 * i], keys[i].bytes.data(), 32);
+    sorted_.emplace_back(keys[i], (uint32_t)i);
+  }
+  std::sort(sorted_.begin(), sorted_.end(),
+            [](const std::pair<PublicKey, uint32_t>& a, const std::pair<PublicKey, uint32_t>& b) { return a.first < b.first; });
+  check(nt_keyset_create(Backend::global().ctx(), pk.data(), (uint32_t)keys.size(), &ks_), "nt_keyset_create");
+}
+
+KeySet::~KeySet() {
+  if (ks_) nt_keyset_free(ks_);
+}
+
+uint32_t KeySet::index_of(const PublicKey& pk) const {
+  auto it = std::lower_bound(sorted_.begin(), sorted_.end(), pk,
+                             [](const std::pair<PublicKey, uint32_t>& a, const PublicKey& b) { return a.first < b; });
+  return (it != sorted_.end() && it->first == pk) ? it->second : UINT32_MAX;
+}
+
+std::vector<bool> KeySet::verify_many(const std::vector<Digest>& digests, const std::vector<PublicKey>& keys,
+                                      const std::vector<Signature>& sigs) const {
+  const size_t n = digests.size();
+  if (keys.size() != n || sigs.size() != n) throw std::invalid_argument("length mismatch");
+  std::vector<bool> out(n, false);
+  if (!n) return out;
+  std::vector<uint32_t> idx(n);
+  std::vector<uint8_t> sg(64 * n), msg(32 * n);
+  std::vector<uint64_t> off(n), len(n, 32);
+  for (size_t i = 0; i < n; ++i) {
+    idx[i] = index_of(keys[i]);
+    const auto f = sigs[i].flatten();
+    std::memcpy(&sg[64 * i], f.data(), 64);
+    std::memcpy(&msg[32 * i], digests[i].bytes.data(), 32);
+    off[i] = 32 * i;
+  }
+  std::vector<uint8_t> bm((n + 7) / 8);
+  check(nt_ed25519_verify_keyset(Backend::global().ctx(), ks_, NT_MODE_STRICT, idx.data(), sg.data(), msg.data(),
+                                 off.data(), len.data(), n, bm.data()),
+        "nt_ed25519_verify_keyset");
+  for (size_t i = 0; i < n; ++i) out[i] = (bm[i / 8] >> (i % 8)) & 1;
+  return out;
+}
+
+std::vector<bool> KeySet::verify_batch_many(
+    const std::vector<Digest>& digests,
+    const std::vector<const std::vector<std::pair<PublicKey, Signature>>*>& groups) const {
+  const size_t G = groups.size();
+  if (digests.size() != G) throw std::invalid_argument("length mismatch");
+  std::vector<bool> out(G, true);
+  if (!G) return out;
+  std::vector<uint32_t> idx;
+  std::vector<uint8_t> sg, msg(32 * G);
+  std::vector<uint64_t> first(G);
+  std::vector<uint32_t> cnt(G);
+  for (size_t g = 0; g < G; ++g) {
+    first[g] = idx.size();
+    cnt[g] = (uint32_t)groups[g]->size();
+    std::memcpy(&msg[32 * g], digests[g].bytes.data(), 32);
+    for (const auto& kv : *groups[g]) {
+      idx.push_back(index_of(kv.first));
+      const auto f = kv.second.flatten();
+      sg.insert(sg.end(), f.begin(), f.end());
+    }
+  }
+  idx.resize(std::max<size_t>(idx.size(), 1));
+  sg.resize(std::max<size_t>(sg.size(), 64));
+  std::vector<uint8_t> bm((G + 7) / 8);
+  check(nt_ed25519_verify_batch_groups_keyset(Backend::global().ctx(), ks_, idx.data(), sg.data(), first.data(),
+                                              cnt.data(), msg.data(), G, bm.data(), nullptr),
+        "nt_ed25519_verify_batch_groups_keyset");
+  for (size_t g = 0; g < G; ++g) out[g] = (bm[g / 8] >> (g % 8)) & 1;
+  return out;
 }
 
 SignatureService::SignatureService(SecretKey secret) : secret_(std::move(secret)) {

@@ -29,6 +29,7 @@
 #include <vector>
 
 struct nt_ctx;
+struct nt_keyset;
 
 namespace crypto {
 
@@ -130,6 +131,32 @@ std::vector<bool> verify_many(const std::vector<Digest>& digests, const std::vec
 std::vector<bool> verify_batch_many(
     const std::vector<Digest>& digests,
     const std::vector<const std::vector<std::pair<PublicKey, Signature>>*>& groups);
+
+// Committee key cache (nt_keyset): per-key comb tables on every device.  Keys
+// are addressed by their index in `keys`; verification against a key that is
+// not in the set rejects (as an unknown PublicKey would fail later checks).
+class KeySet {
+ public:
+  explicit KeySet(const std::vector<PublicKey>& keys);
+  ~KeySet();
+  KeySet(const KeySet&) = delete;
+  KeySet& operator=(const KeySet&) = delete;
+  // index of `pk`, or UINT32_MAX if absent
+  uint32_t index_of(const PublicKey& pk) const;
+  size_t size() const { return keys_.size(); }
+  // verify_strict of (digest_i, key_i, sig_i) for keys in the set
+  std::vector<bool> verify_many(const std::vector<Digest>& digests, const std::vector<PublicKey>& keys,
+                                const std::vector<Signature>& sigs) const;
+  // verify_batch per group, all signers looked up in the set
+  std::vector<bool> verify_batch_many(
+      const std::vector<Digest>& digests,
+      const std::vector<const std::vector<std::pair<PublicKey, Signature>>*>& groups) const;
+
+ private:
+  std::vector<PublicKey> keys_;
+  std::vector<std::pair<PublicKey, uint32_t>> sorted_;
+  ::nt_keyset* ks_ = nullptr;
+};
 
 class SignatureService {
  public:

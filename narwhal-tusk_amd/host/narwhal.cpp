@@ -154,7 +154,14 @@ DagError Certificate::verify(const Committee& committee) const {
   return DagError::Ok;
 }
 
-std::vector<DagError> verify_certificates(const Committee& committee, const std::vector<Certificate>& certs) {
+std::unique_ptr<crypto::KeySet> committee_keyset(const Committee& committee) {
+  std::vector<PublicKey> keys;
+  for (const auto& kv : committee.authorities) keys.push_back(kv.first);
+  return std::make_unique<crypto::KeySet>(keys);
+}
+
+std::vector<DagError> verify_certificates(const Committee& committee, const std::vector<Certificate>& certs,
+                                          const crypto::KeySet* cache) {
   const size_t n = certs.size();
   std::vector<DagError> res(n, DagError::Ok);
   if (!n) return res;
@@ -185,7 +192,7 @@ std::vector<DagError> verify_certificates(const Committee& committee, const std:
     hk.push_back(certs[i].header.author);
     hs.push_back(certs[i].header.signature);
   }
-  const auto hv = crypto::verify_many(hd, hk, hs);
+  const auto hv = cache ? cache->verify_many(hd, hk, hs) : crypto::verify_many(hd, hk, hs);
   // 4) quorum, then every remaining certificate's votes in one verify_batch launch
   std::vector<size_t> grp_idx;
   std::vector<Digest> gd;
@@ -205,7 +212,7 @@ std::vector<DagError> verify_certificates(const Committee& committee, const std:
     gd.push_back(dig[n + i]);
     groups.push_back(&certs[i].votes);
   }
-  const auto gv = crypto::verify_batch_many(gd, groups);
+  const auto gv = cache ? cache->verify_batch_many(gd, groups) : crypto::verify_batch_many(gd, groups);
   for (size_t t = 0; t < grp_idx.size(); ++t)
     if (!gv[t]) res[grp_idx[t]] = DagError::InvalidSignature;
   return res;

@@ -14,6 +14,7 @@
 #pragma once
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <optional>
 #include <set>
 #include <string>
@@ -95,7 +96,12 @@ struct Certificate {
 
 // Verify many certificates with two GPU launches (header signatures, vote
 // groups) plus one digest launch; same verdicts as Certificate::verify each.
-std::vector<DagError> verify_certificates(const Committee& committee, const std::vector<Certificate>& certs);
+// With `cache` (the committee's KeySet) both launches use the
+// per-key comb tables instead of decompressing every public key.
+std::vector<DagError> verify_certificates(const Committee& committee, const std::vector<Certificate>& certs,
+                                          const crypto::KeySet* cache = nullptr);
+// KeySet over the committee's authorities (BTreeMap order).
+std::unique_ptr<crypto::KeySet> committee_keyset(const Committee& committee);
 
 }  // namespace primary
 

@@ -5,6 +5,7 @@
 //   primary/src/tests/core_tests.rs, common.rs (header / votes / certificates)
 // plus negative cases for every DagError the verify paths can return.
 // Usage: test_narwhal <pk0_hex> <pk1_hex> <pk2_hex> <pk3_hex>   (golden keys())
+#include <climits>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -326,10 +327,38 @@ TEST(certificate_errors_and_batched_agreement) {
                            DagError::InvalidSignature, DagError::InvalidSignature, DagError::InvalidSignature,
                            DagError::UnknownAuthority};
   const auto batched = primary::verify_certificates(c, certs);
+  const auto cache = primary::committee_keyset(c);
+  const auto cached = primary::verify_certificates(c, certs, cache.get());
   for (size_t i = 0; i < certs.size(); ++i) {
     CHECK(certs[i].verify(c) == want[i]);
     CHECK(batched[i] == want[i]);
+    CHECK(cached[i] == want[i]);
   }
+}
+
+TEST(committee_keyset_index_and_verify) {
+  const Committee c = committee();
+  const auto cache = primary::committee_keyset(c);
+  CHECK(cache->size() == 4);
+  PublicKey stranger;
+  stranger.bytes[5] = 7;
+  CHECK(cache->index_of(stranger) == UINT32_MAX);
+  const auto k = keys();
+  const Digest d = digest_of("Hello, world!");
+  std::vector<Digest> ds;
+  std::vector<PublicKey> ks;
+  std::vector<Signature> ss;
+  for (const auto& kp : k) {
+    ds.push_back(d);
+    ks.push_back(kp.first);
+    ss.push_back(Signature::new_(d, kp.second));
+  }
+  ds.push_back(d);
+  ks.push_back(stranger);  // not a committee key -> reject
+  ss.push_back(ss[0]);
+  const auto v = cache->verify_many(ds, ks, ss);
+  for (int i = 0; i < 4; ++i) CHECK(v[i]);
+  CHECK(!v[4]);
 }
 
 int main(int argc, char** argv) {
@@ -357,6 +386,7 @@ int main(int argc, char** argv) {
     RUN(header_errors);
     RUN(vote_errors);
     RUN(certificate_errors_and_batched_agreement);
+    RUN(committee_keyset_index_and_verify);
   } catch (const std::exception& e) {
     std::printf("exception: %s\n", e.what());
     return 3;
