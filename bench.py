@@ -171,11 +171,14 @@ def main():
     # algorithmic multiply-accumulates per verify (counted by tests/cpp/opcount)
     mads = mads_per_verify(L)
     achieved = mads * n / (kernel_ms * 1e-3) / 1e12
-    prof = load_profile("r01_verify_pmc.json")
+    prof = load_profile(os.path.join("r01", "pmc_cfg2.json"))
+    pv = (prof or {}).get("kernels", {}).get("verify", {})
     roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": round(MAD_PEAK_TS, 2),
                 "unit": "Tmad/s (v_mad_u64_u32 32x32->64 multiply-accumulates)",
                 "frac": round(achieved / MAD_PEAK_TS, 4),
-                "traffic": prof.get("hbm_bytes_per_launch") if prof else None,
+                "traffic": pv.get("hbm_bytes_per_launch"),
+                "traffic_note": "HBM bytes per launch from rocprofv3 FETCH_SIZE*2 + WRITE_SIZE (profiles/r01/pmc_cfg2.json, "
+                                "same kernel build); algorithmic input is 608 B/verify" if pv else None,
                 "kernel": "k_ed25519_verify<strict>", "kernel_ms": round(kernel_ms, 3),
                 "mads_per_verify": mads}
 
