@@ -1,14 +1,15 @@
 // ed25519_ops.hpp -- per-lane Ed25519 operations shared by the gfx950 kernels
-// (kernels.hip) and the host-compiled bound/op-count harness (tools/opcount.cpp,
-// tests/cpp/).  Table storage is abstracted:
-//   ATab: store(entry, ge_cached) / load(entry, ge_cached&)   -- j*(-A), j = 0..8
-//   BTab: load(idx, ge_niels&)                                 -- j*B,   j = 0..128
+// (kernels.hip) and the host-compiled harness (tests/cpp/nt_host_harness.cpp,
+// tools/opcount.py).  Table storage is abstracted:
+//   ATab:  store(entry, ge_cached) / load(entry, ge_cached&)    j*(-A), j = 0..8, per lane
+//   WComb: load(pos, idx, ge_niels&)                            idx * 2^(16 pos) * P (wide comb)
 //
 // Semantics (restated from ed25519-dalek 1.0.1 /
 // curve25519-dalek 3.x):
-//   verify_one<kStrict>       = PublicKey::verify_strict  (crypto/src/lib.rs:200-204)
-//   verify_one<kCofactorless> = one entry of verify_batch under the deterministic
+//   verify_n<kStrict>         = PublicKey::verify_strict  (crypto/src/lib.rs:200-204)
+//   verify_n<kCofactorless>   = one entry of verify_batch under the deterministic
 //                               rule A.3                   (crypto/src/lib.rs:206-219)
+//   verify_cached_n<..>       = the same two predicates against a committee key cache
 //   sign_one                  = Keypair::generate + sign   (crypto/src/lib.rs:163-191)
 #pragma once
 #include "fe25519.hpp"
@@ -18,368 +19,247 @@
 
 namespace nt {
 
-// [j]B as an affine-niels entry (j = 0 -> identity).
-NT_HD NT_INLINE void btab_entry(ge_niels& q, uint32_t j) {
-  if (j == 0) {
-    ge_niels_0(q);
-    return;
-  }
-  uint32_t enc[8];
-  for (int i = 0; i < 8; ++i) enc[i] = kBaseEnc[i];
-  ge_p3 B, P;
-  ge_frombytes_w(B, enc);
-  ge_cached Bc;
-  ge_p3_to_cached(Bc, B);
-  ge_p3_0(P);
-  for (int bit = 7; bit >= 0; --bit) {
-    ge_p2 t2;
+// a[j] for a loop index j without indexing a per-lane array dynamically (which
+// would put the array in scratch memory): N-way select
+template <int N, class T>
+NT_HD NT_INLINE T pick(const T* a, int j) {
+  T r = a[0];
+#pragma unroll
+  for (int q = 1; q < N; ++q)
+    if (q == j) r = a[q];
+  return r;
+}
+
+// 8 little-endian words from a 16-byte aligned pointer
+NT_HD NT_INLINE void ld8(uint32_t w[8], const uint32_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint4* q = (const uint4*)p;
+  const uint4 a = q[0], b = q[1];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+#else
+  for (int i = 0; i < 8; ++i) w[i] = p[i];
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// Wide combs: for a fixed point P, entry (i, j) = j * 2^(16 i) * P as affine
+// niels, i in [0, 16), j in [0, 2^15].  [x]P is then 16 mixed additions and no
+// doublings (signed radix-2^16 digits of x).  67 MB per point: sized for the
+// MI355X's 288 GB of HBM -- one comb of B per device, one per committee key.
+// ---------------------------------------------------------------------------
+constexpr int kWPos = 16;
+constexpr int kWEntries = 32769;   // |digit| in 0..2^15
+constexpr int kWStride = 32;       // words per entry (30 used)
+constexpr int kWChunk = 64;        // consecutive entries built by one thread
+constexpr int kWChunks = 512;      // chunks per position: entries 1..32768
+
+// acc += [x]P with P's wide comb.  The table load of digit i+1 is issued right
+// after the multiplies that consume entry i, so its latency (a random 128-B
+// line) overlaps the rest of the addition.
+template <class WComb>
+NT_HD NT_INLINE void wcomb_acc(ge_p3& acc, const uint32_t x[8], const WComb& wc) {
+  uint32_t d[8];
+  sc_recode_w16(d, x);
+  int32_t dg = (int32_t)(int16_t)(uint16_t)(d[0] & 0xffffu);
+  ge_niels ne;
+  wc.load(0, (uint32_t)(dg < 0 ? -dg : dg), ne);
+#pragma unroll 1
+  for (int pos = 0; pos < kWPos; ++pos) {
+#pragma unroll
+    for (int m = 0; m < 7; ++m) d[m] = (d[m] >> 16) | (d[m + 1] << 16);
+    d[7] >>= 16;
+    ge_niels_cneg(ne, dg < 0);
+    fe PP, MM, TT;
+    ge_add_niels_1(PP, MM, TT, acc, ne);
+    const int32_t dn = (int32_t)(int16_t)(uint16_t)(d[0] & 0xffffu);
+    const int nxt = pos + 1 < kWPos ? pos + 1 : pos;  // last round reloads a valid entry
+    wc.load(nxt, (uint32_t)(dn < 0 ? -dn : dn), ne);
+    dg = dn;
     ge_cp t;
-    ge_p3_to_p2(t2, P);
-    ge_dbl(t, t2);
+    ge_add_niels_2(t, PP, MM, TT, acc.Z);
+    ge_cp_to_p3(acc, t);
+  }
+}
+
+// Wide-comb construction, step 1 (one thread per point): P_i = 2^(16 i) P,
+// stored as p3 limbs [i][X,Y,Z,T][10].
+NT_HD NT_INLINE void wcomb_bases(uint32_t* out, const ge_p3& P0) {
+  ge_p3 P = P0;
+#pragma unroll 1
+  for (int i = 0; i < kWPos; ++i) {
+    uint32_t* o = out + 40 * i;
+#pragma unroll
+    for (int l = 0; l < 10; ++l) {
+      o[l] = P.X.v[l]; o[10 + l] = P.Y.v[l]; o[20 + l] = P.Z.v[l]; o[30 + l] = P.T.v[l];
+    }
+    ge_p2 q;
+    ge_p3_to_p2(q, P);
+#pragma unroll 1
+    for (int r = 0; r < 15; ++r) ge_dbl_p2(q, q);
+    ge_cp t;
+    ge_dbl(t, q);
     ge_cp_to_p3(P, t);
-    if ((j >> bit) & 1) {
-      ge_add_cached(t, P, Bc);
-      ge_cp_to_p3(P, t);
-    }
-  }
-  fe zi, x, y, d2;
-  fe_invert(zi, P.Z);
-  fe_mul(x, P.X, zi);
-  fe_mul(y, P.Y, zi);
-  fe_add(q.ypx, y, x);
-  fe_carry(q.ypx);
-  fe_sub(q.ymx, y, x);
-  fe_carry(q.ymx);
-  fe_const(d2, kFeD2);
-  fe_mul(q.xy2d, x, y);
-  fe_mul(q.xy2d, q.xy2d, d2);
-}
-
-// acc = [s]B + [k](-A): 64 signed 4-bit windows of k, 32 signed 8-bit windows of s.
-// Every lane follows the same schedule (no divergence).
-template <class ATab, class BTab>
-NT_HD NT_INLINE void ladder(ge_p2& acc, const uint32_t kd[8], const uint32_t sd[8], const ATab& at,
-                            const BTab& bt) {
-  uint32_t kw[8], sw[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) { kw[i] = kd[i]; sw[i] = sd[i]; }
-  ge_p2_0(acc);
-  ge_cp t;
-  ge_p3 u;
-#pragma unroll 1
-  for (int wi = 7; wi >= 0; --wi) {
-    const uint32_t kcur = kw[7], scur = sw[7];
-#pragma unroll
-    for (int m = 7; m > 0; --m) { kw[m] = kw[m - 1]; sw[m] = sw[m - 1]; }
-#pragma unroll 1
-    for (int j = 7; j >= 0; --j) {
-#pragma unroll 1
-      for (int r = 0; r < 3; ++r) ge_dbl_p2(acc, acc);
-      ge_dbl(t, acc);
-      ge_cp_to_p3(u, t);
-      const int32_t dk = (int32_t)(((kcur >> (4 * j)) & 15u) ^ 8u) - 8;
-      const uint32_t negk = dk < 0;
-      ge_cached ce;
-      at.load((uint32_t)(negk ? -dk : dk), ce);
-      ge_cached_cneg(ce, negk);
-      ge_add_cached(t, u, ce);
-      if ((j & 1) == 0) {
-        const int32_t ds = (int32_t)(((scur >> (4 * j)) & 255u) ^ 128u) - 128;
-        const uint32_t negs = ds < 0;
-        ge_niels ne;
-        bt.load((uint32_t)(negs ? -ds : ds), ne);
-        ge_niels_cneg(ne, negs);
-        ge_cp_to_p3(u, t);
-        ge_add_niels(t, u, ne);
-      }
-      ge_cp_to_p2(acc, t);
-    }
   }
 }
 
-// Fixed-base [x]B (x < L) with 8-bit signed windows.
-template <class BTab>
-NT_HD NT_INLINE void base_mul(ge_p2& acc, const uint32_t x[8], const BTab& bt) {
-  uint32_t sd[8];
-  sc_recode_w8(sd, x);
-  ge_p2_0(acc);
-  ge_cp t;
-  ge_p3 u;
-#pragma unroll 1
-  for (int wi = 7; wi >= 0; --wi) {
-    const uint32_t scur = sd[7];
+// Step 2 (one thread per (position, chunk)): entries j0 .. j0+63 of position i
+// with j0 = 1 + 64 c, written to dst (entry j0 first, kWStride words each);
+// chunk 0 also writes entry 0 (identity) at dst - kWStride.  One inversion per
+// chunk (Montgomery's trick); tmp holds the 64 prefix products (640 words).
+NT_HD NT_INLINE void wcomb_fill(uint32_t* dst, uint32_t* tmp, const uint32_t* base, uint32_t c) {
+  ge_p3 P;
 #pragma unroll
-    for (int m = 7; m > 0; --m) sd[m] = sd[m - 1];
-#pragma unroll 1
-    for (int j = 3; j >= 0; --j) {
-#pragma unroll 1
-      for (int r = 0; r < 7; ++r) ge_dbl_p2(acc, acc);
-      ge_dbl(t, acc);
-      ge_cp_to_p3(u, t);
-      const int32_t ds = (int32_t)(((scur >> (8 * j)) & 255u) ^ 128u) - 128;
-      const uint32_t negs = ds < 0;
-      ge_niels ne;
-      bt.load((uint32_t)(negs ? -ds : ds), ne);
-      ge_niels_cneg(ne, negs);
-      ge_add_niels(t, u, ne);
-      ge_cp_to_p2(acc, t);
-    }
-  }
-}
-
-// One verification. Aw = pk words, Rw/Sw = signature halves, msg/len = message.
-// Order chosen to keep little state live across the ladder: A is decoded and
-// checked first; R is only decoded after the ladder (its bytes are 8 words).
-template <int MODE, class ATab, class BTab>
-NT_HD NT_INLINE uint32_t verify_one(const uint32_t Aw[8], const uint32_t Rw[8], const uint32_t Sw[8],
-                                    const uint8_t* msg, uint64_t len, ATab& at, const BTab& bt) {
-  uint32_t ok = sc_is_canonical(Sw);
-  {
-    ge_p3 A;
-    ok &= ge_frombytes_w(A, Aw);
-    if (MODE == kStrict) ok &= ge_is_small_order(A) ^ 1u;
-    // table j * (-A), j = 0..8
-    ge_p3 An;
-    fe_neg(An.X, A.X);
-    fe_carry(An.X);
-    An.Y = A.Y;
-    An.Z = A.Z;
-    fe_neg(An.T, A.T);
-    fe_carry(An.T);
-    ge_cached c0, c1;
-    ge_cached_0(c0);
-    at.store(0, c0);
-    ge_p3_to_cached(c1, An);
-    at.store(1, c1);
-    ge_p3 cur = An;
-#pragma unroll 1
-    for (uint32_t j = 2; j < 9; ++j) {
-      ge_cp t;
-      ge_add_cached(t, cur, c1);
-      ge_cp_to_p3(cur, t);
-      ge_cached cj;
-      ge_p3_to_cached(cj, cur);
-      at.store(j, cj);
-    }
-  }
-  uint32_t kd[8], sd[8];
-  {
-    // k = SHA-512(R || A || M) mod L over the raw encodings (Scalar::from_hash)
-    uint32_t prefix[16];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) { prefix[q] = Rw[q]; prefix[8 + q] = Aw[q]; }
-    uint64_t st[8];
-    sha512_prefixed<16>(st, prefix, msg, len);
-    uint32_t hw[16], k[8];
-    sha512_out_words(hw, st, 16);
-    sc_reduce512(k, hw);
-    sc_recode_w4(kd, k);
-    sc_recode_w8(sd, Sw);
-  }
-  ge_p2 Rp;
-  ladder(Rp, kd, sd, at, bt);
-  ge_p3 R;
-  ok &= ge_frombytes_w(R, Rw);
-  if (MODE == kStrict) ok &= ge_is_small_order(R) ^ 1u;
-  ok &= ge_eq_affine(Rp, R);
-  return ok;
-}
-
-// Keygen + RFC 8032 signature.  sw = 32-byte seed words.
-template <class BTab>
-NT_HD NT_INLINE void sign_one(uint32_t Aw[8], uint32_t Rw[8], uint32_t s[8], const uint32_t sw[8],
-                              const uint8_t* msg, uint64_t len, const BTab& bt) {
-  uint64_t st[8];
-  sha512_prefixed<8>(st, sw, nullptr, 0);
-  uint32_t h[16];
-  sha512_out_words(h, st, 16);
-  uint32_t a[8], pre[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) { a[q] = h[q]; pre[q] = h[8 + q]; }
-  a[0] &= 0xfffffff8u;
-  a[7] &= 0x3fffffffu;
-  a[7] |= 0x40000000u;
-  uint32_t ared[8];
-  sc_reduce256(ared, a);
-  ge_p2 P;
-  base_mul(P, ared, bt);
-  ge_tobytes_w(Aw, P);
-
-  sha512_prefixed<8>(st, pre, msg, len);
-  uint32_t hr[16], r[8];
-  sha512_out_words(hr, st, 16);
-  sc_reduce512(r, hr);
-  base_mul(P, r, bt);
-  ge_tobytes_w(Rw, P);
-
-  uint32_t prefix[16];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) { prefix[q] = Rw[q]; prefix[8 + q] = Aw[q]; }
-  sha512_prefixed<16>(st, prefix, msg, len);
-  uint32_t hk[16], k[8];
-  sha512_out_words(hk, st, 16);
-  sc_reduce512(k, hk);
-  sc_muladd(s, k, a, r);
-}
-
-}  // namespace nt
-
-namespace nt {
-
-// ---------------------------------------------------------------------------
-// Committee key cache: fixed-base combs.
-//   comb entry (i, j) = j * 256^i * P  as affine niels, i in [0, 32), j in [0, 128]
-// With a comb for -A and one for B, [s]B + [k](-A) is 64 mixed additions and
-// no doublings: 32 signed 8-bit digits of k and of s.
-// ---------------------------------------------------------------------------
-constexpr int kCombPos = 32;
-constexpr int kCombEntries = 129;
-
-// j * 256^i * P (P given as p3), returned affine-niels.
-NT_HD NT_INLINE void comb_entry(ge_niels& q, const ge_p3& P, uint32_t i, uint32_t j) {
-  if (j == 0) {
-    ge_niels_0(q);
-    return;
+  for (int l = 0; l < 10; ++l) {
+    P.X.v[l] = base[l]; P.Y.v[l] = base[10 + l]; P.Z.v[l] = base[20 + l]; P.T.v[l] = base[30 + l];
   }
   ge_cached Pc;
   ge_p3_to_cached(Pc, P);
+  // Q = j0 * P by double-and-add over the 16 bits of j0
+  const uint32_t j0 = 1u + (uint32_t)kWChunk * c;
   ge_p3 Q;
   ge_p3_0(Q);
   ge_cp t;
 #pragma unroll 1
-  for (int bit = 7; bit >= 0; --bit) {
-    ge_p2 t2;
-    ge_p3_to_p2(t2, Q);
-    ge_dbl(t, t2);
+  for (int bit = 15; bit >= 0; --bit) {
+    ge_p2 q2;
+    ge_p3_to_p2(q2, Q);
+    ge_dbl(t, q2);
     ge_cp_to_p3(Q, t);
-    if ((j >> bit) & 1) {
+    if ((j0 >> bit) & 1u) {
       ge_add_cached(t, Q, Pc);
       ge_cp_to_p3(Q, t);
     }
   }
-  ge_p2 q2;
-  ge_p3_to_p2(q2, Q);
+  // forward: projective X,Y,Z into the entry slots, prefix products of Z in tmp
+  fe acc;
 #pragma unroll 1
-  for (uint32_t r = 0; r < 8 * i; ++r) ge_dbl_p2(q2, q2);
-  fe zi, x, y, d2;
-  fe_invert(zi, q2.Z);
-  fe_mul(x, q2.X, zi);
-  fe_mul(y, q2.Y, zi);
-  fe_add(q.ypx, y, x);
-  fe_carry(q.ypx);
-  fe_sub(q.ymx, y, x);
-  fe_carry(q.ymx);
-  fe_const(d2, kFeD2);
-  fe_mul(q.xy2d, x, y);
-  fe_mul(q.xy2d, q.xy2d, d2);
+  for (int e = 0; e < kWChunk; ++e) {
+    uint32_t* o = dst + (size_t)e * kWStride;
+#pragma unroll
+    for (int l = 0; l < 10; ++l) { o[l] = Q.X.v[l]; o[10 + l] = Q.Y.v[l]; o[20 + l] = Q.Z.v[l]; }
+    if (e == 0) acc = Q.Z;
+    else fe_mul(acc, acc, Q.Z);
+#pragma unroll
+    for (int l = 0; l < 10; ++l) tmp[10 * e + l] = acc.v[l];
+    ge_add_cached(t, Q, Pc);
+    ge_cp_to_p3(Q, t);
+  }
+  fe inv;
+  fe_invert(inv, acc);
+  // backward: Z_e^-1 = inv * prefix_{e-1}; inv *= Z_e
+#pragma unroll 1
+  for (int e = kWChunk - 1; e >= 0; --e) {
+    uint32_t* o = dst + (size_t)e * kWStride;
+    fe X, Y, Z, zi;
+#pragma unroll
+    for (int l = 0; l < 10; ++l) { X.v[l] = o[l]; Y.v[l] = o[10 + l]; Z.v[l] = o[20 + l]; }
+    if (e > 0) {
+      fe pre;
+#pragma unroll
+      for (int l = 0; l < 10; ++l) pre.v[l] = tmp[10 * (e - 1) + l];
+      fe_mul(zi, inv, pre);
+      fe_mul(inv, inv, Z);
+    } else {
+      zi = inv;
+    }
+    ge_niels q;
+    ge_niels_from(q, X, Y, zi);
+#pragma unroll
+    for (int l = 0; l < 10; ++l) { o[l] = q.ypx.v[l]; o[10 + l] = q.ymx.v[l]; o[20 + l] = q.xy2d.v[l]; }
+    o[30] = 0;
+    o[31] = 0;
+  }
+  if (c == 0) {
+    uint32_t* o = dst - kWStride;
+    ge_niels z;
+    ge_niels_0(z);
+#pragma unroll
+    for (int l = 0; l < 10; ++l) { o[l] = z.ypx.v[l]; o[10 + l] = z.ymx.v[l]; o[20 + l] = z.xy2d.v[l]; }
+    o[30] = 0;
+    o[31] = 0;
+  }
 }
 
-// Key metadata bits produced at keyset build time.
-enum : uint32_t { kKeyDecodes = 1u, kKeySmallOrder = 2u };
+// ---------------------------------------------------------------------------
+// Variable-base part: [k](-A) with 4-bit signed windows over a per-lane table
+// ---------------------------------------------------------------------------
 
-// One verification against a cached key.  CA: comb of -A, CB: comb of B;
-// both expose load(pos, idx, ge_niels&).  meta: kKey* bits of the key.
-template <int MODE, class CombA, class CombB>
-NT_HD NT_INLINE uint32_t verify_one_cached(uint32_t meta, const uint32_t Aw[8], const uint32_t Rw[8],
-                                           const uint32_t Sw[8], const uint8_t* msg, uint64_t len,
-                                           const CombA& ca, const CombB& cb) {
-  uint32_t ok = sc_is_canonical(Sw) & (meta & kKeyDecodes ? 1u : 0u);
-  if (MODE == kStrict) ok &= (meta & kKeySmallOrder) ? 0u : 1u;
-  uint32_t kd[8], sd[8];
-  {
-    uint32_t prefix[16];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) { prefix[q] = Rw[q]; prefix[8 + q] = Aw[q]; }
-    uint64_t st[8];
-    sha512_prefixed<16>(st, prefix, msg, len);
-    uint32_t hw[16], k[8];
-    sha512_out_words(hw, st, 16);
-    sc_reduce512(k, hw);
-    sc_recode_w8(kd, k);
-    sc_recode_w8(sd, Sw);
-  }
-  ge_p3 acc;
-  ge_p3_0(acc);
-  ge_cp t;
-  // word w of kd/sd holds the digits of positions 4w..4w+3 (one byte each);
-  // consume word 0 and shift the arrays down (no dynamic register indexing)
+// Decode A (dalek decompress), strict: reject small order; store j * (-A), j = 0..8.
+template <int MODE, class ATab>
+NT_HD NT_INLINE uint32_t atab_build(const uint32_t Aw[8], ATab& at) {
+  ge_p3 A;
+  uint32_t ok = ge_frombytes_w(A, Aw);
+  if (MODE == kStrict) ok &= ge_is_small_order(A) ^ 1u;
+  ge_p3 An;
+  fe_neg(An.X, A.X);
+  fe_carry(An.X);
+  An.Y = A.Y;
+  An.Z = A.Z;
+  fe_neg(An.T, A.T);
+  fe_carry(An.T);
+  ge_cached c0, c1;
+  ge_cached_0(c0);
+  at.store(0, c0);
+  ge_p3_to_cached(c1, An);
+  at.store(1, c1);
+  ge_p3 cur = An;
 #pragma unroll 1
-  for (int w = 0; w < 8; ++w) {
-    const uint32_t kw = kd[0], sw = sd[0];
-#pragma unroll
-    for (int m = 0; m < 7; ++m) { kd[m] = kd[m + 1]; sd[m] = sd[m + 1]; }
-#pragma unroll 1
-    for (int b = 0; b < 4; ++b) {
-      const uint32_t pos = 4 * w + b;
-      const int32_t dk = (int32_t)(((kw >> (8 * b)) & 255u) ^ 128u) - 128;
-      const int32_t ds = (int32_t)(((sw >> (8 * b)) & 255u) ^ 128u) - 128;
-      ge_niels ne;
-      ca.load(pos, (uint32_t)(dk < 0 ? -dk : dk), ne);
-      ge_niels_cneg(ne, dk < 0);
-      ge_add_niels(t, acc, ne);
-      ge_cp_to_p3(acc, t);
-      cb.load(pos, (uint32_t)(ds < 0 ? -ds : ds), ne);
-      ge_niels_cneg(ne, ds < 0);
-      ge_add_niels(t, acc, ne);
-      ge_cp_to_p3(acc, t);
-    }
+  for (uint32_t j = 2; j < 9; ++j) {
+    ge_cp t;
+    ge_add_cached(t, cur, c1);
+    ge_cp_to_p3(cur, t);
+    ge_cached cj;
+    ge_p3_to_cached(cj, cur);
+    at.store(j, cj);
   }
-  ge_p3 R;
-  ok &= ge_frombytes_w(R, Rw);
-  if (MODE == kStrict) ok &= ge_is_small_order(R) ^ 1u;
-  ge_p2 Rp;
-  ge_p3_to_p2(Rp, acc);
-  ok &= ge_eq_affine(Rp, R);
   return ok;
 }
 
-}  // namespace nt
-
-namespace nt {
-
-// ---------------------------------------------------------------------------
-// Cached verification of TWO signatures per lane with one shared inversion.
-//
-// R is never decompressed.  For R' = [s]B - [k]A with affine (x', y'):
-//   dalek accepts  <=>  R decodes to a point equal to R'
-//                  <=>  y_R == y' (mod p)  and  (sign(R) == parity(x')  or  x' == 0)
-// (R's y is taken mod p exactly as curve25519-dalek's from_bytes does; a valid
-// R' makes R decodable whenever y matches; x' = 0 covers the accepted
-// "negative zero" encodings).  In strict mode the small-order test of R is done
-// on R' (equal points have equal order; if they differ the verdict is reject
-// anyway).  The two Z^-1 come from one exponentiation (Montgomery's trick).
-// ---------------------------------------------------------------------------
-template <class CombA, class CombB>
-NT_HD NT_INLINE void comb_ladder(ge_p3& acc, const uint32_t k[8], const uint32_t Sw[8], const CombA& ca,
-                                 const CombB& cb) {
-  uint32_t kd[8], sd[8];
-  sc_recode_w8(kd, k);
-  sc_recode_w8(sd, Sw);
-  ge_p3_0(acc);
-  ge_cp t;
-#pragma unroll 1
-  for (int w = 0; w < 8; ++w) {
-    const uint32_t kw = kd[0], sw = sd[0];
+// t = [k](-A) (completed) for k < 2^253 given as 64 signed 4-bit digits.
+// The top digit seeds the accumulator (no doublings of the identity): 252
+// doublings and 63 additions.  Every lane follows the same schedule.
+template <class ATab>
+NT_HD NT_INLINE void ladder_a(ge_cp& t, const uint32_t kd[8], const ATab& at) {
+  uint32_t kw[8];
 #pragma unroll
-    for (int m = 0; m < 7; ++m) { kd[m] = kd[m + 1]; sd[m] = sd[m + 1]; }
+  for (int i = 0; i < 8; ++i) kw[i] = kd[i];
+  {
+    const int32_t d = (int32_t)((kw[7] >> 28) ^ 8u) - 8;
+    ge_cached ce;
+    at.load((uint32_t)(d < 0 ? -d : d), ce);
+    ge_cached_cneg(ce, d < 0);
+    // cached (Y+X, Y-X, 2Z, .) -> (2X : 2Y : 2Z) as a completed point with T = Z
+    fe_sub(t.X, ce.YpX, ce.YmX);
+    fe_carry(t.X);
+    fe_add(t.Y, ce.YpX, ce.YmX);
+    fe_carry(t.Y);
+    t.Z = ce.Z2;
+    t.T = ce.Z2;
+  }
 #pragma unroll 1
-    for (int b = 0; b < 4; ++b) {
-      const uint32_t pos = 4 * w + b;
-      const int32_t dk = (int32_t)(((kw >> (8 * b)) & 255u) ^ 128u) - 128;
-      const int32_t ds = (int32_t)(((sw >> (8 * b)) & 255u) ^ 128u) - 128;
-      ge_niels ne;
-      ca.load(pos, (uint32_t)(dk < 0 ? -dk : dk), ne);
-      ge_niels_cneg(ne, dk < 0);
-      ge_add_niels(t, acc, ne);
-      ge_cp_to_p3(acc, t);
-      cb.load(pos, (uint32_t)(ds < 0 ? -ds : ds), ne);
-      ge_niels_cneg(ne, ds < 0);
-      ge_add_niels(t, acc, ne);
-      ge_cp_to_p3(acc, t);
+  for (int wi = 7; wi >= 0; --wi) {
+    const uint32_t cur = kw[7];
+#pragma unroll
+    for (int m = 7; m > 0; --m) kw[m] = kw[m - 1];
+#pragma unroll 1
+    for (int j = (wi == 7 ? 6 : 7); j >= 0; --j) {
+      ge_p2 acc;
+      ge_cp_to_p2(acc, t);
+#pragma unroll 1
+      for (int r = 0; r < 3; ++r) ge_dbl_p2(acc, acc);
+      ge_dbl(t, acc);
+      const int32_t dk = (int32_t)(((cur >> (4 * j)) & 15u) ^ 8u) - 8;
+      ge_cached ce;
+      at.load((uint32_t)(dk < 0 ? -dk : dk), ce);  // latency overlaps the conversion
+      ge_p3 u;
+      ge_cp_to_p3(u, t);
+      ge_cached_cneg(ce, dk < 0);
+      ge_add_cached(t, u, ce);
     }
   }
 }
 
+// k = SHA-512(R || A || M) mod L over the raw encodings (Scalar::from_hash)
 NT_HD NT_INLINE void hram_scalar(uint32_t k[8], const uint32_t Rw[8], const uint32_t Aw[8], const uint8_t* msg,
                                  uint64_t len) {
   uint32_t prefix[16];
@@ -392,7 +272,17 @@ NT_HD NT_INLINE void hram_scalar(uint32_t k[8], const uint32_t Rw[8], const uint
   sc_reduce512(k, hw);
 }
 
-// compare affine (x, y) with the encoding Rw under dalek decode semantics
+// ---------------------------------------------------------------------------
+// Final comparison without decompressing R.  For R' = [s]B - [k]A with affine
+// (x', y'):
+//   dalek accepts  <=>  R decodes to a point equal to R'
+//                  <=>  y_R == y' (mod p)  and  (sign(R) == parity(x')  or  x' == 0)
+// (R's y is taken mod p exactly as curve25519-dalek's from_bytes does; a valid
+// R' makes R decodable whenever y matches; x' = 0 covers the accepted
+// "negative zero" encodings).  In strict mode the small-order test of R is done
+// on R' (equal points have equal order; if they differ the verdict is reject
+// anyway).  With N = 2 the two Z^-1 come from one inversion (Montgomery's trick).
+// ---------------------------------------------------------------------------
 NT_HD NT_INLINE uint32_t enc_matches(const fe& x, const fe& y, const uint32_t Rw[8]) {
   fe yr;
   fe_frombytes_w(yr, Rw);  // bit 255 dropped, value taken mod p by the compare
@@ -410,35 +300,141 @@ NT_HD NT_INLINE uint32_t enc_matches(const fe& x, const fe& y, const uint32_t Rw
   return same & (((xw[0] & 1u) == sign) | (xz == 0));
 }
 
-template <int MODE, class CombA, class CombB>
-NT_HD NT_INLINE void verify_two_cached(uint32_t ok[2], const uint32_t meta[2], const uint32_t Aw[2][8],
-                                       const uint32_t Rw[2][8], const uint32_t Sw[2][8], const uint8_t* msg[2],
-                                       const uint64_t len[2], const CombA ca[2], const CombB& cb) {
-  ge_p2 P[2];
-#pragma unroll 1
-  for (int j = 0; j < 2; ++j) {
-    ok[j] = sc_is_canonical(Sw[j]) & (meta[j] & kKeyDecodes ? 1u : 0u);
-    if (MODE == kStrict) ok[j] &= (meta[j] & kKeySmallOrder) ? 0u : 1u;
-    uint32_t k[8];
-    hram_scalar(k, Rw[j], Aw[j], msg[j], len[j]);
-    ge_p3 acc;
-    comb_ladder(acc, k, Sw[j], ca[j], cb);
-    ge_p3_to_p2(P[j], acc);
+template <int MODE, int N>
+NT_HD NT_INLINE void finish_compare(uint32_t ok[N], const ge_p2 P[N], const uint32_t* const sig[N]) {
+  static_assert(N == 1 || N == 2, "one or two signatures per lane");
+  fe zi[N];
+  if (N == 1) {
+    fe_invert(zi[0], P[0].Z);
+  } else {
+    fe zz, inv;
+    fe_mul(zz, P[0].Z, P[N - 1].Z);
+    fe_invert(inv, zz);
+    fe_mul(zi[0], inv, P[N - 1].Z);
+    fe_mul(zi[N - 1], inv, P[0].Z);
   }
-  // Z0^-1, Z1^-1 from one inversion
-  fe zz, inv, zi0, zi1;
-  fe_mul(zz, P[0].Z, P[1].Z);
-  fe_invert(inv, zz);
-  fe_mul(zi0, inv, P[1].Z);
-  fe_mul(zi1, inv, P[0].Z);
-#pragma unroll 1
-  for (int j = 0; j < 2; ++j) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
     fe x, y;
-    fe_mul(x, P[j].X, j ? zi1 : zi0);
-    fe_mul(y, P[j].Y, j ? zi1 : zi0);
-    ok[j] &= enc_matches(x, y, Rw[j]);
+    fe_mul(x, P[j].X, zi[j]);
+    fe_mul(y, P[j].Y, zi[j]);
+    uint32_t Rw[8];
+    ld8(Rw, sig[j]);
+    ok[j] &= enc_matches(x, y, Rw);
     if (MODE == kStrict) ok[j] &= ge_is_small_order_p2(P[j]) ^ 1u;
   }
+}
+
+// N (1 or 2) verifications per lane.  A[j] = 8 pk words, sig[j] = 16 words
+// (R || s), msg[j]/len[j] = message.  at is this lane's j*(-A) table (reused
+// by the N signatures in turn), wb the wide comb of B.
+template <int MODE, int N, class ATab, class WComb>
+NT_HD NT_INLINE void verify_n(uint32_t ok[N], const uint32_t* const A[N], const uint32_t* const sig[N],
+                              const uint8_t* const msg[N], const uint64_t len[N], ATab& at, const WComb& wb) {
+  ge_p2 P[N];
+#pragma unroll 1
+  for (int j = 0; j < N; ++j) {
+    const uint32_t* sj = pick<N>(sig, j);
+    uint32_t Aw[8], Sw[8], kd[8];
+    ld8(Aw, pick<N>(A, j));
+    ld8(Sw, sj + 8);
+    uint32_t okj = sc_is_canonical(Sw);
+    okj &= atab_build<MODE>(Aw, at);
+    {
+      uint32_t Rw[8], k[8];
+      ld8(Rw, sj);
+      hram_scalar(k, Rw, Aw, pick<N>(msg, j), pick<N>(len, j));
+      sc_recode_w4(kd, k);
+    }
+    ge_cp t;
+    ladder_a(t, kd, at);
+    ge_p3 acc;
+    ge_cp_to_p3(acc, t);
+    wcomb_acc(acc, Sw, wb);
+    // keep the first result in registers (select, not a dynamically indexed array)
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      if (q == j) {
+        ge_p3_to_p2(P[q], acc);
+        ok[q] = okj;
+      }
+    }
+  }
+  finish_compare<MODE, N>(ok, P, sig);
+}
+
+// Key-cache variant: ca[j] is the wide comb of -A_j, meta[j] its kKey* bits.
+enum : uint32_t { kKeyDecodes = 1u, kKeySmallOrder = 2u };
+
+template <int MODE, int N, class WCombA, class WCombB>
+NT_HD NT_INLINE void verify_cached_n(uint32_t ok[N], const uint32_t meta[N], const uint32_t* const A[N],
+                                     const uint32_t* const sig[N], const uint8_t* const msg[N],
+                                     const uint64_t len[N], const WCombA ca[N], const WCombB& cb) {
+  ge_p2 P[N];
+#pragma unroll 1
+  for (int j = 0; j < N; ++j) {
+    const uint32_t* sj = pick<N>(sig, j);
+    const uint32_t mj = pick<N>(meta, j);
+    uint32_t Aw[8], Sw[8], k[8];
+    ld8(Aw, pick<N>(A, j));
+    ld8(Sw, sj + 8);
+    uint32_t okj = sc_is_canonical(Sw) & (mj & kKeyDecodes ? 1u : 0u);
+    if (MODE == kStrict) okj &= (mj & kKeySmallOrder) ? 0u : 1u;
+    {
+      uint32_t Rw[8];
+      ld8(Rw, sj);
+      hram_scalar(k, Rw, Aw, pick<N>(msg, j), pick<N>(len, j));
+    }
+    ge_p3 acc;
+    ge_p3_0(acc);
+    wcomb_acc(acc, k, pick<N>(ca, j));
+    wcomb_acc(acc, Sw, cb);
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      if (q == j) {
+        ge_p3_to_p2(P[q], acc);
+        ok[q] = okj;
+      }
+    }
+  }
+  finish_compare<MODE, N>(ok, P, sig);
+}
+
+// Keygen + RFC 8032 signature.  sw = 32-byte seed words; wb = wide comb of B.
+template <class WComb>
+NT_HD NT_INLINE void sign_one(uint32_t Aw[8], uint32_t Rw[8], uint32_t s[8], const uint32_t sw[8],
+                              const uint8_t* msg, uint64_t len, const WComb& wb) {
+  uint64_t st[8];
+  sha512_prefixed<8>(st, sw, nullptr, 0);
+  uint32_t h[16];
+  sha512_out_words(h, st, 16);
+  uint32_t a[8], pre[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) { a[q] = h[q]; pre[q] = h[8 + q]; }
+  a[0] &= 0xfffffff8u;
+  a[7] &= 0x3fffffffu;
+  a[7] |= 0x40000000u;
+  uint32_t ared[8];
+  sc_reduce256(ared, a);
+  ge_p3 P;
+  ge_p2 P2;
+  ge_p3_0(P);
+  wcomb_acc(P, ared, wb);
+  ge_p3_to_p2(P2, P);
+  ge_tobytes_w(Aw, P2);
+
+  sha512_prefixed<8>(st, pre, msg, len);
+  uint32_t hr[16], r[8];
+  sha512_out_words(hr, st, 16);
+  sc_reduce512(r, hr);
+  ge_p3_0(P);
+  wcomb_acc(P, r, wb);
+  ge_p3_to_p2(P2, P);
+  ge_tobytes_w(Rw, P2);
+
+  uint32_t k[8];
+  hram_scalar(k, Rw, Aw, msg, len);
+  sc_muladd(s, k, a, r);
 }
 
 }  // namespace nt

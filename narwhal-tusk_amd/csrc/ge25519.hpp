@@ -89,18 +89,42 @@ NT_HD NT_INLINE void ge_add_cached(ge_cp& r, const ge_p3& p, const ge_cached& q)
   fe_sub(r.T, ZZ, TT);
 }
 
-NT_HD NT_INLINE void ge_add_niels(ge_cp& r, const ge_p3& p, const ge_niels& q) {
-  fe a, b, PP, MM, TT, ZZ;
+// P + Q, Q affine niels.  Split in two halves so a caller can issue its next
+// table load as soon as the multiplies that read q have been issued.
+NT_HD NT_INLINE void ge_add_niels_1(fe& PP, fe& MM, fe& TT, const ge_p3& p, const ge_niels& q) {
+  fe a, b;
   fe_add(a, p.Y, p.X);
   fe_sub(b, p.Y, p.X);
   fe_mul(PP, a, q.ypx);
   fe_mul(MM, b, q.ymx);
   fe_mul(TT, p.T, q.xy2d);
-  fe_add(ZZ, p.Z, p.Z);       // < 2^27
+}
+NT_HD NT_INLINE void ge_add_niels_2(ge_cp& r, const fe& PP, const fe& MM, const fe& TT, const fe& Z) {
+  fe ZZ;
+  fe_add(ZZ, Z, Z);           // < 2^27
   fe_sub(r.X, PP, MM);
   fe_add(r.Y, PP, MM);
   fe_add(r.Z, ZZ, TT);
   fe_sub(r.T, ZZ, TT);        // ZZ + 2p - TT < 2^27.6
+}
+NT_HD NT_INLINE void ge_add_niels(ge_cp& r, const ge_p3& p, const ge_niels& q) {
+  fe PP, MM, TT;
+  ge_add_niels_1(PP, MM, TT, p, q);
+  ge_add_niels_2(r, PP, MM, TT, p.Z);
+}
+
+// Affine niels entry of the projective point (X:Y:Z), given zi = Z^-1.
+NT_HD NT_INLINE void ge_niels_from(ge_niels& q, const fe& X, const fe& Y, const fe& zi) {
+  fe x, y, d2;
+  fe_mul(x, X, zi);
+  fe_mul(y, Y, zi);
+  fe_add(q.ypx, y, x);
+  fe_carry(q.ypx);
+  fe_sub(q.ymx, y, x);
+  fe_carry(q.ymx);
+  fe_const(d2, kFeD2);
+  fe_mul(q.xy2d, x, y);
+  fe_mul(q.xy2d, q.xy2d, d2);
 }
 
 // Conditionally negate a cached entry in place: -(Y+X, Y-X, 2Z, 2dT) = (Y-X, Y+X, 2Z, -2dT)

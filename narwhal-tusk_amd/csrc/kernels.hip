@@ -2,21 +2,23 @@
 //
 //   k_sha512_trunc32      one lane per message, Digest = SHA-512[..32]
 //                         (worker/src/processor.rs:38; primary/src/messages.rs:70-84,145-153,226-234)
-//   k_ed25519_verify<M>   one lane per signature; M = strict (crypto/src/lib.rs:200-204 ->
+//   k_ed25519_verify<M>   two signatures per lane; M = strict (crypto/src/lib.rs:200-204 ->
 //                         dalek verify_strict) or cofactorless (per-entry rule of
 //                         crypto/src/lib.rs:206-219 -> dalek verify_batch);
 //                         writes one verdict bit per signature (64-bit ballot words)
+//   k_ed25519_verify_keyset<M>  the same against a committee key cache (wide combs of -A)
 //   k_group_and           AND of per-signature bits over each certificate's vote range
 //   k_ed25519_sign        keygen + RFC 8032 signing (corpus generation / SignatureService
 //                         batch form; crypto/src/lib.rs:163-191) -- not constant time
-//   k_btab_init           [j]B, j = 0..128, affine-niels table (built once per device)
+//   k_wcomb_bases/fill    wide-comb construction (B once per device, committee keys)
 //
 // SIMT design: every lane runs the same window schedule (fixed signed windows,
 // never per-lane sliding windows), so lanes of a wave never diverge inside the
-// double-scalar ladder.  [s]B uses 8-bit windows over a 129-entry affine table
-// staged in LDS (16.5 KiB per workgroup); [k](-A) uses 4-bit windows over a
-// per-lane 9-entry cached table in a global workspace laid out lane-minor so
-// each lane's 16-byte accesses coalesce across the workgroup.
+// scalar multiplications.  [s]B is 16 mixed additions from the 67 MB wide comb
+// of B (random 128-byte lines, the next one prefetched during the current
+// addition); [k](-A) uses 4-bit windows over a per-lane 9-entry cached table in
+// a global workspace laid out lane-minor so each lane's 16-byte accesses
+// coalesce across the workgroup.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -27,8 +29,6 @@
 namespace nt {
 
 constexpr int kBlock = 256;
-constexpr int kBEntries = 129;        // |digit| in 0..128
-constexpr int kBStride = 32;          // words per niels entry (30 used)
 constexpr int kAEntries = 9;          // |digit| in 0..8
 constexpr int kAQuads = 10;           // uint4 per cached entry (40 words)
 
@@ -51,32 +51,13 @@ __global__ __launch_bounds__(kBlock) void k_sha512_trunc32(const uint8_t* __rest
 }
 
 // --------------------------------------------------------------------------
-// Base-point table: one thread per entry j = 0..128
-// --------------------------------------------------------------------------
-__global__ void k_btab_init(uint32_t* __restrict__ tab) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= kBEntries) return;
-  ge_niels q;
-  btab_entry(q, (uint32_t)j);
-  uint32_t* dst = tab + (size_t)j * kBStride;
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    dst[i] = q.ypx.v[i];
-    dst[10 + i] = q.ymx.v[i];
-    dst[20 + i] = q.xy2d.v[i];
-  }
-  dst[30] = 0;
-  dst[31] = 0;
-}
-
-// --------------------------------------------------------------------------
 // Table accessors
 // --------------------------------------------------------------------------
-// [j]B entries staged in LDS, 32 words per entry (8 x ds_read_b128).
-struct LdsBTab {
-  const uint32_t* lds;
-  NT_D NT_INLINE void load(uint32_t idx, ge_niels& q) const {
-    const uint4* e = (const uint4*)(lds + idx * kBStride);
+// Wide comb of one point, layout [pos][entry][32 words]; 8 x 16-byte loads.
+struct WideComb {
+  const uint32_t* base;
+  NT_D NT_INLINE void load(uint32_t pos, uint32_t idx, ge_niels& q) const {
+    const uint4* e = (const uint4*)(base + ((size_t)pos * kWEntries + idx) * kWStride);
     uint32_t w[32];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -91,6 +72,8 @@ struct LdsBTab {
     }
   }
 };
+
+constexpr size_t kWWordsPerKey = (size_t)kWPos * kWEntries * kWStride;
 
 // j*(-A) entries in the global workspace, layout [slot][entry][quad][lane] of
 // uint4: a lane's 16-byte accesses are adjacent to its neighbours'.
@@ -126,109 +109,89 @@ struct WsATab {
   }
 };
 
-NT_D NT_INLINE void load_btab_lds(uint32_t* lds, const uint32_t* __restrict__ btab_g) {
-  const uint4* src = (const uint4*)btab_g;
-  uint4* dst = (uint4*)lds;
-  for (int i = threadIdx.x; i < kBEntries * kBStride / 4; i += kBlock) dst[i] = src[i];
-  __syncthreads();
-}
-
-NT_D NT_INLINE void load8(uint32_t w[8], const uint32_t* __restrict__ p) {
-  const uint4* q = (const uint4*)p;
-  const uint4 a = q[0], b = q[1];
-  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
-}
-
 // --------------------------------------------------------------------------
-// Verification: one lane per signature, grid-stride over workspace slots
+// Wide-comb construction
 // --------------------------------------------------------------------------
-template <int MODE, int OCC>
-__global__ __launch_bounds__(kBlock, OCC) void k_ed25519_verify(
-    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
-    const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t n,
-    const uint32_t* __restrict__ btab_g, uint4* __restrict__ ws,
-    unsigned long long* __restrict__ out_bits) {
-  __shared__ __attribute__((aligned(16))) uint32_t btab[kBEntries * kBStride];
-  load_btab_lds(btab, btab_g);
-  const LdsBTab bt{btab};
-  WsATab at{ws, blockIdx.x};
-  for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < n; base += (uint64_t)gridDim.x * kBlock) {
-    const uint64_t gi = base + threadIdx.x;
-    const uint32_t active = gi < n;
-    const uint64_t i = active ? gi : n - 1;
-    uint32_t Aw[8], Rw[8], Sw[8];
-    load8(Aw, pk + 8 * i);
-    load8(Rw, sig + 16 * i);
-    load8(Sw, sig + 16 * i + 8);
-    const uint32_t ok = active & verify_one<MODE>(Aw, Rw, Sw, msg + off[i], len[i], at, bt);
-    const unsigned long long bal = __ballot(ok);
-    const uint64_t wbase = base + (threadIdx.x & ~63u);
-    if ((threadIdx.x & 63u) == 0 && wbase < n) out_bits[wbase >> 6] = bal;
-  }
-}
-
-// --------------------------------------------------------------------------
-// Committee key cache: comb tables  [pos][key][entry][32 words]
-// --------------------------------------------------------------------------
-// One thread per (key, pos, entry).  sign_neg = 1 builds the comb of -P (keys),
-// 0 the comb of P itself (the base point).  meta[key] gets kKey* bits.
-__global__ void k_comb_build(const uint32_t* __restrict__ enc, uint32_t nkeys, int negate,
-                             uint32_t* __restrict__ comb, uint32_t* __restrict__ meta) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t per_key = (uint64_t)kCombPos * kCombEntries;
-  if (t >= per_key * nkeys) return;
-  const uint32_t key = (uint32_t)(t / per_key);
-  const uint32_t pos = (uint32_t)((t % per_key) / kCombEntries);
-  const uint32_t j = (uint32_t)(t % kCombEntries);
+// One thread per point: decode (or take B), optionally negate, write the 16
+// bases 2^(16 i) P.  meta[key] gets the kKey* bits.  Keys that do not decode get
+// identity bases (every entry the identity; such keys always reject via meta).
+__global__ void k_wcomb_bases(const uint32_t* __restrict__ enc, uint32_t nkeys, int negate,
+                              uint32_t* __restrict__ bases, uint32_t* __restrict__ meta) {
+  const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
+  if (key >= nkeys) return;
   uint32_t w[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) w[i] = enc[8 * key + i];
   ge_p3 P;
   const uint32_t ok = ge_frombytes_w(P, w);
-  if (pos == 0 && j == 0 && meta) meta[key] = (ok ? kKeyDecodes : 0u) | (ge_is_small_order(P) ? kKeySmallOrder : 0u);
+  if (meta) meta[key] = (ok ? kKeyDecodes : 0u) | (ge_is_small_order(P) ? kKeySmallOrder : 0u);
+  if (!ok) ge_p3_0(P);
   if (negate) {
     fe_neg(P.X, P.X);
     fe_carry(P.X);
     fe_neg(P.T, P.T);
     fe_carry(P.T);
   }
-  ge_niels q;
-  if (ok) comb_entry(q, P, pos, j);
-  else ge_niels_0(q);
-  uint32_t* dst = comb + (((uint64_t)pos * nkeys + key) * kCombEntries + j) * kBStride;
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    dst[i] = q.ypx.v[i];
-    dst[10 + i] = q.ymx.v[i];
-    dst[20 + i] = q.xy2d.v[i];
-  }
-  dst[30] = 0;
-  dst[31] = 0;
+  wcomb_bases(bases + (size_t)key * kWPos * 40, P);
 }
 
-struct GlobalComb {
-  const uint32_t* comb;
-  uint32_t nkeys, key;
-  NT_D NT_INLINE void load(uint32_t pos, uint32_t idx, ge_niels& q) const {
-    const uint4* e = (const uint4*)(comb + (((uint64_t)pos * nkeys + key) * kCombEntries + idx) * kBStride);
-    uint32_t w[32];
+// One thread per (key, position, chunk of 64 entries).
+__global__ void k_wcomb_fill(const uint32_t* __restrict__ bases, uint32_t nkeys, uint32_t* __restrict__ comb,
+                             uint32_t* __restrict__ tmp) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t per_key = (uint64_t)kWPos * kWChunks;
+  if (t >= per_key * nkeys) return;
+  const uint32_t key = (uint32_t)(t / per_key);
+  const uint32_t pos = (uint32_t)((t % per_key) / kWChunks);
+  const uint32_t c = (uint32_t)(t % kWChunks);
+  uint32_t* dst = comb + key * kWWordsPerKey + ((size_t)pos * kWEntries + 1 + (size_t)kWChunk * c) * kWStride;
+  wcomb_fill(dst, tmp + t * (kWChunk * 10), bases + ((size_t)key * kWPos + pos) * 40, c);
+}
+
+// --------------------------------------------------------------------------
+// Verification: two signatures per lane, grid-stride over workspace slots.
+// Block iteration covers 512 signatures; wave w, lane l, slot j handles
+// signature base + 128 w + 64 j + l (so each verdict word is one ballot).
+// --------------------------------------------------------------------------
+template <int MODE, int OCC>
+__global__ __launch_bounds__(kBlock, OCC) void k_ed25519_verify(
+    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+    const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t n,
+    const uint32_t* __restrict__ combB, uint4* __restrict__ ws, unsigned long long* __restrict__ out_bits) {
+  WsATab at{ws, blockIdx.x};
+  const WideComb wb{combB};
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wofs = 128 * (uint64_t)(threadIdx.x >> 6);
+  for (uint64_t base = (uint64_t)blockIdx.x * 2 * kBlock; base < n; base += (uint64_t)gridDim.x * 2 * kBlock) {
+    uint32_t act[2];
+    const uint32_t* A[2];
+    const uint32_t* S[2];
+    const uint8_t* M[2];
+    uint64_t L[2];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint4 v = e[i];
-      w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+    for (int j = 0; j < 2; ++j) {
+      const uint64_t gi = base + wofs + 64 * j + lane;
+      act[j] = gi < n;
+      const uint64_t i = act[j] ? gi : n - 1;
+      A[j] = pk + 8 * i;
+      S[j] = sig + 16 * i;
+      M[j] = msg + off[i];
+      L[j] = len[i];
     }
+    uint32_t ok[2];
+    verify_n<MODE, 2>(ok, A, S, M, L, at, wb);
 #pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      q.ypx.v[i] = w[i];
-      q.ymx.v[i] = w[10 + i];
-      q.xy2d.v[i] = w[20 + i];
+    for (int j = 0; j < 2; ++j) {
+      const unsigned long long bal = __ballot(ok[j] & act[j]);
+      const uint64_t wbase = base + wofs + 64 * j;
+      if (lane == 0 && wbase < n) out_bits[wbase >> 6] = bal;
     }
   }
-};
+}
 
-// Verification against a cached committee: each lane verifies TWO signatures
-// (wave w, lane l: signatures 128w + l and 128w + 64 + l) sharing one field
-// inversion; key_idx[i] selects the key (>= nkeys -> unknown key -> reject).
+// Verification against a cached committee: two signatures per lane (wave w,
+// lane l: signatures 128w + l and 128w + 64 + l); key_idx[i] selects the key
+// (>= nkeys -> unknown key -> reject).
 template <int MODE>
 __global__ __launch_bounds__(kBlock, 2) void k_ed25519_verify_keyset(
     const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
@@ -237,10 +200,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_ed25519_verify_keyset(
     uint32_t nkeys, const uint32_t* __restrict__ combB, unsigned long long* __restrict__ out_bits) {
   const uint64_t wave = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63u;
-  uint32_t act[2], m[2], Aw[2][8], Rw[2][8], Sw[2][8];
-  const uint8_t* mp[2];
-  uint64_t ml[2];
-  GlobalComb ca[2];
+  uint32_t act[2], m[2];
+  const uint32_t* A[2];
+  const uint32_t* S[2];
+  const uint8_t* M[2];
+  uint64_t L[2];
+  WideComb ca[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const uint64_t gi = 128 * wave + 64 * j + lane;
@@ -249,17 +214,16 @@ __global__ __launch_bounds__(kBlock, 2) void k_ed25519_verify_keyset(
     const uint32_t kraw = key_idx[i];
     const uint32_t known = kraw < nkeys;
     const uint32_t key = known ? kraw : 0u;
-    load8(Aw[j], enc + 8 * key);
-    load8(Rw[j], sig + 16 * i);
-    load8(Sw[j], sig + 16 * i + 8);
+    A[j] = enc + 8 * key;
+    S[j] = sig + 16 * i;
     m[j] = known ? meta[key] : 0u;
-    mp[j] = msg + off[i];
-    ml[j] = len[i];
-    ca[j] = GlobalComb{combA, nkeys, key};
+    M[j] = msg + off[i];
+    L[j] = len[i];
+    ca[j] = WideComb{combA + key * kWWordsPerKey};
   }
-  const GlobalComb cb{combB, 1u, 0u};
+  const WideComb cb{combB};
   uint32_t ok[2];
-  verify_two_cached<MODE>(ok, m, Aw, Rw, Sw, mp, ml, ca, cb);
+  verify_cached_n<MODE, 2>(ok, m, A, S, M, L, ca, cb);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const unsigned long long bal = __ballot(ok[j] & act[j]);
@@ -301,22 +265,20 @@ __global__ __launch_bounds__(kBlock) void k_ed25519_sign(const uint32_t* __restr
                                                         const uint8_t* __restrict__ msg,
                                                         const uint64_t* __restrict__ off,
                                                         const uint64_t* __restrict__ len, uint64_t n,
-                                                        const uint32_t* __restrict__ btab_g,
+                                                        const uint32_t* __restrict__ combB,
                                                         uint32_t* __restrict__ out_pk,
                                                         uint32_t* __restrict__ out_sig) {
-  __shared__ __attribute__((aligned(16))) uint32_t btab[kBEntries * kBStride];
-  load_btab_lds(btab, btab_g);
-  const LdsBTab bt{btab};
+  const WideComb wb{combB};
   for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < n; base += (uint64_t)gridDim.x * kBlock) {
     const uint64_t gi = base + threadIdx.x;
     const uint32_t active = gi < n;
     const uint64_t i = active ? gi : n - 1;
     uint32_t sw[8];
-    load8(sw, seed + 8 * i);
+    ld8(sw, seed + 8 * i);
     uint32_t Aw[8], Rw[8], s[8];
     const uint8_t* m = msg ? msg + off[i] : nullptr;
     const uint64_t ml = msg ? len[i] : 0;
-    sign_one(Aw, Rw, s, sw, m, ml, bt);
+    sign_one(Aw, Rw, s, sw, m, ml, wb);
     if (active) {
       uint4* po = (uint4*)(out_pk + 8 * i);
       po[0] = make_uint4(Aw[0], Aw[1], Aw[2], Aw[3]);
@@ -335,11 +297,6 @@ __global__ __launch_bounds__(kBlock) void k_ed25519_sign(const uint32_t* __restr
 // --------------------------------------------------------------------------
 // Launchers (host)
 // --------------------------------------------------------------------------
-hipError_t launch_btab_init(uint32_t* d_tab, hipStream_t s) {
-  hipLaunchKernelGGL(k_btab_init, dim3((kBEntries + 63) / 64), dim3(64), 0, s, d_tab);
-  return hipGetLastError();
-}
-
 hipError_t launch_sha512_trunc32(const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
                                  uint64_t n, uint8_t* d_out32, hipStream_t s) {
   if (n == 0) return hipSuccess;
@@ -350,8 +307,8 @@ hipError_t launch_sha512_trunc32(const uint8_t* d_data, const uint64_t* d_off, c
 }
 
 // Occupancy variant of the verify kernel (waves per SIMD the register
-// allocator targets): 1 = no spills, 2 = twice the latency hiding with some
-// scratch.  NT_VERIFY_OCC selects at run time (A/B measurement); default 2.
+// allocator targets).  NT_VERIFY_OCC selects at run time (A/B measurement);
+// default 2.
 static int verify_occ() {
   static int occ = [] {
     const char* e = std::getenv("NT_VERIFY_OCC");
@@ -363,29 +320,29 @@ static int verify_occ() {
 template <int MODE>
 static void launch_verify_mode(uint64_t blocks, const uint8_t* d_pk, const uint8_t* d_sig,
                                const uint8_t* d_msg, const uint64_t* d_off, const uint64_t* d_len,
-                               uint64_t n, const uint32_t* d_btab, void* d_ws, uint64_t* d_out_words,
+                               uint64_t n, const uint32_t* d_combB, void* d_ws, uint64_t* d_out_words,
                                hipStream_t s) {
   if (verify_occ() == 1)
     hipLaunchKernelGGL((k_ed25519_verify<MODE, 1>), dim3((uint32_t)blocks), dim3(kBlock), 0, s,
-                       (const uint32_t*)d_pk, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_btab,
+                       (const uint32_t*)d_pk, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_combB,
                        (uint4*)d_ws, (unsigned long long*)d_out_words);
   else
     hipLaunchKernelGGL((k_ed25519_verify<MODE, 2>), dim3((uint32_t)blocks), dim3(kBlock), 0, s,
-                       (const uint32_t*)d_pk, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_btab,
+                       (const uint32_t*)d_pk, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_combB,
                        (uint4*)d_ws, (unsigned long long*)d_out_words);
 }
 
 hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
                          const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
-                         const uint32_t* d_btab, void* d_ws, uint32_t ws_slots, uint64_t* d_out_words,
+                         const uint32_t* d_combB, void* d_ws, uint32_t ws_slots, uint64_t* d_out_words,
                          hipStream_t s) {
   if (n == 0) return hipSuccess;
-  uint64_t blocks = (n + kBlock - 1) / kBlock;
+  uint64_t blocks = (n + 2 * kBlock - 1) / (2 * kBlock);  // two signatures per lane
   if (blocks > ws_slots) blocks = ws_slots;
   if (mode == kStrict)
-    launch_verify_mode<kStrict>(blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_btab, d_ws, d_out_words, s);
+    launch_verify_mode<kStrict>(blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_combB, d_ws, d_out_words, s);
   else
-    launch_verify_mode<kCofactorless>(blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_btab, d_ws,
+    launch_verify_mode<kCofactorless>(blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_combB, d_ws,
                                       d_out_words, s);
   return hipGetLastError();
 }
@@ -400,24 +357,37 @@ hipError_t launch_group_and(const uint64_t* d_first, const uint32_t* d_cnt, uint
 }
 
 hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, const uint64_t* d_off,
-                       const uint64_t* d_len, uint64_t n, const uint32_t* d_btab, uint8_t* d_pk,
+                       const uint64_t* d_len, uint64_t n, const uint32_t* d_combB, uint8_t* d_pk,
                        uint8_t* d_sig, uint32_t max_blocks, hipStream_t s) {
   if (n == 0) return hipSuccess;
   uint64_t blocks = (n + kBlock - 1) / kBlock;
   if (blocks > max_blocks) blocks = max_blocks;
   hipLaunchKernelGGL(k_ed25519_sign, dim3((uint32_t)blocks), dim3(kBlock), 0, s,
-                     (const uint32_t*)d_seed, d_msg, d_off, d_len, n, d_btab, (uint32_t*)d_pk,
+                     (const uint32_t*)d_seed, d_msg, d_off, d_len, n, d_combB, (uint32_t*)d_pk,
                      (uint32_t*)d_sig);
   return hipGetLastError();
 }
 
-hipError_t launch_comb_build(const uint32_t* d_enc, uint32_t nkeys, int negate, uint32_t* d_comb,
-                             uint32_t* d_meta, hipStream_t s) {
-  const uint64_t threads = (uint64_t)nkeys * kCombPos * kCombEntries;
-  if (!threads) return hipSuccess;
-  hipLaunchKernelGGL(k_comb_build, dim3((uint32_t)((threads + 127) / 128)), dim3(128), 0, s, d_enc, nkeys, negate,
-                     d_comb, d_meta);
-  return hipGetLastError();
+// Builds the wide combs of nkeys points, `batch` keys per fill launch (tmp must
+// hold wcomb_fill_tmp_bytes_per_key() * batch bytes; bases nkeys * wcomb_bases_bytes_per_key()).
+hipError_t launch_wcomb_build(const uint32_t* d_enc, uint32_t nkeys, int negate, uint32_t* d_comb,
+                              uint32_t* d_meta, uint32_t* d_bases, uint32_t* d_tmp, uint32_t batch,
+                              hipStream_t s) {
+  if (nkeys == 0) return hipSuccess;
+  if (batch == 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_wcomb_bases, dim3((nkeys + 63) / 64), dim3(64), 0, s, d_enc, nkeys, negate, d_bases,
+                     d_meta);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  for (uint32_t k0 = 0; k0 < nkeys; k0 += batch) {
+    const uint32_t nk = nkeys - k0 < batch ? nkeys - k0 : batch;
+    const uint64_t threads = (uint64_t)nk * kWPos * kWChunks;
+    hipLaunchKernelGGL(k_wcomb_fill, dim3((uint32_t)((threads + 63) / 64)), dim3(64), 0, s,
+                       d_bases + (size_t)k0 * kWPos * 40, nk, d_comb + (size_t)k0 * kWWordsPerKey, d_tmp);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_verify_keyset(int mode, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
@@ -437,9 +407,9 @@ hipError_t launch_verify_keyset(int mode, const uint32_t* d_key_idx, const uint8
   return hipGetLastError();
 }
 
-size_t comb_bytes_per_key() { return (size_t)kCombPos * kCombEntries * kBStride * 4; }
-
-size_t btab_bytes() { return (size_t)kBEntries * kBStride * 4; }
+size_t wcomb_bytes_per_key() { return kWWordsPerKey * 4; }
+size_t wcomb_bases_bytes_per_key() { return (size_t)kWPos * 40 * 4; }
+size_t wcomb_fill_tmp_bytes_per_key() { return (size_t)kWPos * kWChunks * kWChunk * 10 * 4; }
 size_t ws_bytes_per_slot() { return (size_t)kAEntries * kAQuads * kBlock * 16; }
 
 }  // namespace nt

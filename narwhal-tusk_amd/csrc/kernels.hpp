@@ -6,26 +6,27 @@
 
 namespace nt {
 
-hipError_t launch_btab_init(uint32_t* d_tab, hipStream_t s);
 hipError_t launch_sha512_trunc32(const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
                                  uint64_t n, uint8_t* d_out32, hipStream_t s);
 hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
                          const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
-                         const uint32_t* d_btab, void* d_ws, uint32_t ws_slots, uint64_t* d_out_words,
+                         const uint32_t* d_combB, void* d_ws, uint32_t ws_slots, uint64_t* d_out_words,
                          hipStream_t s);
 hipError_t launch_group_and(const uint64_t* d_first, const uint32_t* d_cnt, uint64_t G,
                             const uint64_t* d_sig_words, uint64_t* d_group_words, hipStream_t s);
 hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, const uint64_t* d_off,
-                       const uint64_t* d_len, uint64_t n, const uint32_t* d_btab, uint8_t* d_pk,
+                       const uint64_t* d_len, uint64_t n, const uint32_t* d_combB, uint8_t* d_pk,
                        uint8_t* d_sig, uint32_t max_blocks, hipStream_t s);
-hipError_t launch_comb_build(const uint32_t* d_enc, uint32_t nkeys, int negate, uint32_t* d_comb,
-                             uint32_t* d_meta, hipStream_t s);
+hipError_t launch_wcomb_build(const uint32_t* d_enc, uint32_t nkeys, int negate, uint32_t* d_comb,
+                              uint32_t* d_meta, uint32_t* d_bases, uint32_t* d_tmp, uint32_t batch,
+                              hipStream_t s);
 hipError_t launch_verify_keyset(int mode, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                                 const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                                 const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
                                 const uint32_t* d_combB, uint64_t* d_out_words, hipStream_t s);
-size_t comb_bytes_per_key();
-size_t btab_bytes();
+size_t wcomb_bytes_per_key();
+size_t wcomb_bases_bytes_per_key();
+size_t wcomb_fill_tmp_bytes_per_key();
 size_t ws_bytes_per_slot();
 
 }  // namespace nt

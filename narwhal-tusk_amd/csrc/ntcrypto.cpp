@@ -1,7 +1,8 @@
 // ntcrypto.cpp -- host side of the C ABI (include/ntcrypto.h).
 //
-// Owns one `Device` per GPU: a non-blocking HIP stream, the [j]B table, the
-// per-lane [k]A table workspace and grow-only device/pinned staging buffers.
+// Owns one `Device` per GPU: a non-blocking HIP stream, the wide comb of B
+// (67 MB), the per-lane [k]A table workspace and grow-only device/pinned
+// staging buffers.
 // Host entry points shard items over devices by contiguous index ranges (one
 // host thread per device), stage through pinned memory, launch, and gather the
 // bitmaps / digests.  There is deliberately no CPU compute path: if HIP or the
@@ -25,6 +26,12 @@ namespace {
   do {                                     \
     hipError_t _e = (expr);                \
     if (_e != hipSuccess) return NT_EHIP;  \
+  } while (0)
+
+#define NT_CHK0(expr)             \
+  do {                            \
+    int _rc = (expr);             \
+    if (_rc != NT_OK) return _rc; \
   } while (0)
 
 struct DevBuf {
@@ -68,8 +75,7 @@ enum { B_DATA, B_OFF, B_LEN, B_PK, B_SIG, B_OUT, B_OUT2, B_FIRST, B_CNT, B_NBUF 
 struct Device {
   int ordinal = -1;
   hipStream_t stream = nullptr;
-  uint32_t* d_btab = nullptr;
-  uint32_t* d_combB = nullptr;  // comb of B for the key-cache path
+  uint32_t* d_combB = nullptr;  // wide comb of B (verify, key-cache verify, sign)
   void* d_ws = nullptr;
   uint32_t ws_slots = 0;
   uint32_t sign_blocks = 0;
@@ -86,7 +92,6 @@ struct Device {
       if (b.p) (void)hipFree(b.p);
     for (auto& b : h)
       if (b.p) (void)hipHostFree(b.p);
-    if (d_btab) (void)hipFree(d_btab);
     if (d_combB) (void)hipFree(d_combB);
     if (d_ws) (void)hipFree(d_ws);
     if (ws_done) (void)hipEventDestroy(ws_done);
@@ -101,18 +106,11 @@ struct Device {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NT_ENODEV;
     NT_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     NT_TRY(hipEventCreateWithFlags(&ws_done, hipEventDisableTiming));
-    NT_TRY(hipMalloc(&d_btab, nt::btab_bytes()));
-    NT_TRY(nt::launch_btab_init(d_btab, stream));
     {
-      uint32_t* d_benc = nullptr;
-      NT_TRY(hipMalloc(&d_benc, 32));
       static const uint32_t kB[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                                      0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
-      NT_TRY(hipMemcpyAsync(d_benc, kB, 32, hipMemcpyHostToDevice, stream));
-      NT_TRY(hipMalloc(&d_combB, nt::comb_bytes_per_key()));
-      NT_TRY(nt::launch_comb_build(d_benc, 1, 0, d_combB, nullptr, stream));
-      NT_TRY(hipStreamSynchronize(stream));
-      (void)hipFree(d_benc);
+      if (hipMalloc(&d_combB, nt::wcomb_bytes_per_key()) != hipSuccess) return NT_ENOMEM;
+      NT_CHK0(build_wcombs(kB, 1, 0, d_combB, nullptr));
     }
     // one workspace slot per resident workgroup; default 4 per CU
     uint32_t slots = (uint32_t)prop.multiProcessorCount * 4;
@@ -125,13 +123,36 @@ struct Device {
     return NT_OK;
   }
 
+  // Wide combs of nkeys encoded points (host words) into d_comb (device);
+  // negate: comb of -P (committee keys) instead of P (the base point).
+  int build_wcombs(const uint32_t* enc_host, uint32_t nkeys, int negate, uint32_t* d_comb, uint32_t* d_meta) {
+    if (nkeys == 0) return NT_OK;
+    const uint32_t batch = std::min<uint32_t>(nkeys, 16);
+    uint32_t *d_enc = nullptr, *d_bases = nullptr, *d_tmp = nullptr;
+    int rc = NT_OK;
+    if (hipMalloc(&d_enc, 32ull * nkeys) != hipSuccess ||
+        hipMalloc(&d_bases, nt::wcomb_bases_bytes_per_key() * nkeys) != hipSuccess ||
+        hipMalloc(&d_tmp, nt::wcomb_fill_tmp_bytes_per_key() * batch) != hipSuccess) {
+      rc = NT_ENOMEM;
+    } else if (hipMemcpyAsync(d_enc, enc_host, 32ull * nkeys, hipMemcpyHostToDevice, stream) != hipSuccess ||
+               nt::launch_wcomb_build(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, stream) !=
+                   hipSuccess ||
+               hipStreamSynchronize(stream) != hipSuccess) {
+      rc = NT_EHIP;
+    }
+    if (d_enc) (void)hipFree(d_enc);
+    if (d_bases) (void)hipFree(d_bases);
+    if (d_tmp) (void)hipFree(d_tmp);
+    return rc;
+  }
+
   // verify launch that shares the workspace: wait for the previous user, then mark
   hipError_t verify(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
                     const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out,
                     hipStream_t s) {
     hipError_t e = hipStreamWaitEvent(s, ws_done, 0);
     if (e != hipSuccess) return e;
-    e = nt::launch_verify(mode, pk, sig, msg, off, len, n, d_btab, d_ws, ws_slots, out, s);
+    e = nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, d_ws, ws_slots, out, s);
     if (e != hipSuccess) return e;
     return hipEventRecord(ws_done, s);
   }
@@ -482,7 +503,7 @@ int nt_ed25519_sign_batch(nt_ctx* ctx, const uint8_t* seed32, const uint8_t* msg
     NT_CHK(dv.d[B_SIG].ensure(m * 64));
     NT_CHK(dv.d[B_OUT].ensure(m * 32));
     NT_TRY(hipMemcpyAsync(dv.d[B_OUT].p, seed32 + 32 * lo, m * 32, hipMemcpyHostToDevice, dv.stream));
-    NT_TRY(nt::launch_sign(dv.d[B_OUT].as<uint8_t>(), d_msg, d_off, d_len, m, dv.d_btab,
+    NT_TRY(nt::launch_sign(dv.d[B_OUT].as<uint8_t>(), d_msg, d_off, d_len, m, dv.d_combB,
                            dv.d[B_PK].as<uint8_t>(), sig64 ? dv.d[B_SIG].as<uint8_t>() : nullptr,
                            dv.sign_blocks, dv.stream));
     NT_TRY(hipMemcpyAsync(pk32 + 32 * lo, dv.d[B_PK].p, m * 32, hipMemcpyDeviceToHost, dv.stream));
@@ -515,10 +536,12 @@ int nt_keyset_create(nt_ctx* ctx, const uint8_t* pk32, uint32_t nkeys, nt_keyset
     const size_t nk = std::max<uint32_t>(nkeys, 1);
     if (hipMalloc(&pd.d_enc, 32 * nk) != hipSuccess) return NT_ENOMEM;
     if (hipMalloc(&pd.d_meta, 4 * nk) != hipSuccess) return NT_ENOMEM;
-    if (hipMalloc(&pd.d_comb, nt::comb_bytes_per_key() * nk) != hipSuccess) return NT_ENOMEM;
+    if (hipMalloc(&pd.d_comb, nt::wcomb_bytes_per_key() * nk) != hipSuccess) return NT_ENOMEM;
     if (nkeys) {
       NT_TRY(hipMemcpyAsync(pd.d_enc, pk32, 32ull * nkeys, hipMemcpyHostToDevice, dv.stream));
-      NT_TRY(nt::launch_comb_build(pd.d_enc, nkeys, 1, pd.d_comb, pd.d_meta, dv.stream));
+      NT_TRY(hipStreamSynchronize(dv.stream));
+      const int rc = dv.build_wcombs((const uint32_t*)pk32, nkeys, 1, pd.d_comb, pd.d_meta);
+      if (rc != NT_OK) return rc;
       if (di == 0)
         NT_TRY(hipMemcpyAsync(ks->flags.data(), pd.d_meta, 4ull * nkeys, hipMemcpyDeviceToHost, dv.stream));
     }
@@ -720,7 +743,7 @@ int nt_dev_ed25519_sign(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_see
   if (!dv) return NT_EINVAL;
   NT_TRY(hipSetDevice(dv->ordinal));
   hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
-  NT_TRY(nt::launch_sign(d_seed32, d_msg, d_off, d_len, n, dv->d_btab, d_pk32, d_sig64,
+  NT_TRY(nt::launch_sign(d_seed32, d_msg, d_off, d_len, n, dv->d_combB, d_pk32, d_sig64,
                          dv->sign_blocks, s));
   return NT_OK;
 }

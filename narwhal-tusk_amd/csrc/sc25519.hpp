@@ -144,4 +144,22 @@ NT_HD NT_INLINE void sc_recode_w8(uint32_t out[8], const uint32_t s[8]) {
   }
 }
 
+// Signed radix-2^16 recoding: 16 digits in [-2^15, 2^15) as two's-complement
+// halfwords (digit i in bits 16(i%2).. of word i/2).  Exact for s < 2^255 - 2^239
+// (every scalar < L); for larger s (non-canonical signature scalars, rejected
+// anyway) the final carry is dropped, and every |digit| stays <= 2^15.
+NT_HD NT_INLINE void sc_recode_w16(uint32_t out[8], const uint32_t s[8]) {
+  uint32_t carry = 0;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) {
+    const uint32_t lo = (s[w] & 0xffffu) + carry;
+    carry = lo >= 0x8000u;
+    const uint32_t hi = (s[w] >> 16) + carry;
+    const uint32_t dlo = (lo - (carry << 16)) & 0xffffu;
+    carry = hi >= 0x8000u;
+    const uint32_t dhi = (hi - (carry << 16)) & 0xffffu;
+    out[w] = dlo | (dhi << 16);
+  }
+}
+
 }  // namespace nt

@@ -21,6 +21,7 @@ def load():
         subprocess.run(["make", "-s", "-C", CPP], check=True)
         _lib = ctypes.CDLL(LIB)
         _lib.nth_verify.restype = ctypes.c_int
+        _lib.nth_wcomb_chunk.restype = ctypes.c_uint32
         _lib.nth_count_mul.restype = ctypes.c_ulonglong
         _lib.nth_count_sq.restype = ctypes.c_ulonglong
     return _lib
@@ -62,6 +63,24 @@ def fe_tobytes(f):
 
 def verify(mode, pk, sig, msg):
     return bool(load().nth_verify(mode, pk, sig, msg, ctypes.c_uint64(len(msg))))
+
+
+def verify_pair(mode, pk0, sig0, msg0, pk1, sig1, msg1, cached=False):
+    """Two signatures through the two-per-lane kernel path (shared inversion);
+    cached=True: the committee key-cache path (wide combs of -A)."""
+    out = (ctypes.c_int * 2)()
+    fn = load().nth_verify_cached_pair if cached else load().nth_verify_pair
+    fn(mode, pk0 + pk1, sig0 + sig1, msg0, ctypes.c_uint64(len(msg0)), msg1, ctypes.c_uint64(len(msg1)), out)
+    return bool(out[0]), bool(out[1])
+
+
+def wcomb_chunk(enc, negate, pos, c):
+    """Device wide-comb construction on the host: (meta, 65 x 32 words) for
+    entries 64c .. 64c+64 of position pos (entry 64c only filled when c == 0)."""
+    import numpy as np
+    out = (ctypes.c_uint32 * (65 * 32))()
+    meta = load().nth_wcomb_chunk(enc, negate, pos, c, out)
+    return meta, np.frombuffer(bytes(out), np.uint32).reshape(65, 32)
 
 
 def sign(seed, msg):

@@ -2,11 +2,14 @@
 // narwhal-tusk_amd/csrc/*.hpp compiled for the host (g++, NT_HD empty) so that
 // CPU-only tests can (a) stress the radix-2^25.5 bound discipline with
 // adversarial limb values against Python big integers, (b) replay the golden
-// corpus through the same verify_one<> the kernels run, and (c) count field
-// multiplies per operation (profiles/opcount.json, the roofline numerator).
+// corpus through the same verify_n<> / verify_cached_n<> the kernels run,
+// (c) check the wide-comb construction (wcomb_bases/wcomb_fill) against an
+// independent curve model, and (d) count field multiplies per operation
+// (profiles/opcount.json, the roofline numerator).
 // Never linked into libntcrypto.so.
 #define NT_OPCOUNT 1
 #include <cstring>
+#include <unordered_map>
 
 #include "../../narwhal-tusk_amd/csrc/ed25519_ops.hpp"
 
@@ -22,19 +25,89 @@ struct HostATab {
   void store(uint32_t j, const ge_cached& c) { e[j] = c; }
   void load(uint32_t j, ge_cached& c) const { c = e[j]; }
 };
-struct HostBTab {
-  ge_niels e[129];
-  bool ready = false;
-  void load(uint32_t j, ge_niels& q) const { q = e[j]; }
-};
-HostBTab& btab() {
-  static HostBTab t;
-  if (!t.ready) {
-    for (uint32_t j = 0; j < 129; ++j) btab_entry(t.e[j], j);
-    t.ready = true;
+
+// Wide comb of a point with entries computed on demand (and memoized) by
+// plain double-and-add; table construction is not counted by NT_OPCOUNT.
+struct HostWComb {
+  ge_p3 base[kWPos];
+  mutable std::unordered_map<uint32_t, ge_niels> memo;
+  void init(const ge_p3& P) {
+    const unsigned long long m0 = g_fe_mul, s0 = g_fe_sq;
+    uint32_t w[kWPos * 40];
+    wcomb_bases(w, P);
+    for (int i = 0; i < kWPos; ++i)
+      for (int l = 0; l < 10; ++l) {
+        base[i].X.v[l] = w[40 * i + l];
+        base[i].Y.v[l] = w[40 * i + 10 + l];
+        base[i].Z.v[l] = w[40 * i + 20 + l];
+        base[i].T.v[l] = w[40 * i + 30 + l];
+      }
+    g_fe_mul = m0;
+    g_fe_sq = s0;
   }
-  return t;
+  void load(uint32_t pos, uint32_t idx, ge_niels& q) const {
+    const uint32_t key = (pos << 16) | idx;
+    auto it = memo.find(key);
+    if (it != memo.end()) {
+      q = it->second;
+      return;
+    }
+    const unsigned long long m0 = g_fe_mul, s0 = g_fe_sq;
+    if (idx == 0) {
+      ge_niels_0(q);
+    } else {
+      ge_cached Pc;
+      ge_p3_to_cached(Pc, base[pos]);
+      ge_p3 Q;
+      ge_p3_0(Q);
+      ge_cp t;
+      for (int bit = 15; bit >= 0; --bit) {
+        ge_p2 q2;
+        ge_p3_to_p2(q2, Q);
+        ge_dbl(t, q2);
+        ge_cp_to_p3(Q, t);
+        if ((idx >> bit) & 1u) {
+          ge_add_cached(t, Q, Pc);
+          ge_cp_to_p3(Q, t);
+        }
+      }
+      fe zi;
+      fe_invert(zi, Q.Z);
+      ge_niels_from(q, Q.X, Q.Y, zi);
+    }
+    g_fe_mul = m0;
+    g_fe_sq = s0;
+    memo.emplace(key, q);
+  }
+};
+
+HostWComb& bcomb() {
+  static HostWComb* c = [] {
+    auto* w = new HostWComb;
+    uint32_t enc[8];
+    for (int i = 0; i < 8; ++i) enc[i] = kBaseEnc[i];
+    ge_p3 B;
+    ge_frombytes_w(B, enc);
+    w->init(B);
+    return w;
+  }();
+  return *c;
 }
+
+// kKey* bits and the comb of -A, as k_wcomb_bases builds them
+uint32_t key_comb(HostWComb& c, const uint32_t Aw[8]) {
+  ge_p3 P;
+  const uint32_t ok = ge_frombytes_w(P, Aw);
+  const uint32_t meta = (ok ? kKeyDecodes : 0u) | (ge_is_small_order(P) ? kKeySmallOrder : 0u);
+  if (!ok) ge_p3_0(P);
+  fe_neg(P.X, P.X);
+  fe_carry(P.X);
+  fe_neg(P.T, P.T);
+  fe_carry(P.T);
+  c.init(P);
+  return meta;
+}
+
 void words(uint32_t w[8], const uint8_t* b) { std::memcpy(w, b, 32); }
 }  // namespace
 
@@ -95,23 +168,91 @@ void nth_sha512(const uint8_t* msg, uint64_t len, uint8_t* out64) {
   std::memcpy(out64, w, 64);
 }
 int nth_verify(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint64_t len) {
-  uint32_t A[8], R[8], S[8];
-  words(A, pk);
-  words(R, sig);
-  words(S, sig + 32);
+  alignas(16) uint32_t A[8], S[16];
+  std::memcpy(A, pk, 32);
+  std::memcpy(S, sig, 64);
+  const uint32_t* Ap[1] = {A};
+  const uint32_t* Sp[1] = {S};
+  const uint8_t* Mp[1] = {msg};
+  const uint64_t Lp[1] = {len};
+  uint32_t ok[1];
   HostATab at;
-  if (mode == 0) return (int)verify_one<kStrict>(A, R, S, msg, len, at, btab());
-  return (int)verify_one<kCofactorless>(A, R, S, msg, len, at, btab());
+  if (mode == 0) verify_n<kStrict, 1>(ok, Ap, Sp, Mp, Lp, at, bcomb());
+  else verify_n<kCofactorless, 1>(ok, Ap, Sp, Mp, Lp, at, bcomb());
+  return (int)ok[0];
+}
+// Two signatures through the two-per-lane path the kernel runs (shared inversion).
+void nth_verify_pair(int mode, const uint8_t* pk64, const uint8_t* sig128, const uint8_t* m0, uint64_t l0,
+                     const uint8_t* m1, uint64_t l1, int* out2) {
+  alignas(16) uint32_t A[2][8], S[2][16];
+  std::memcpy(A, pk64, 64);
+  std::memcpy(S, sig128, 128);
+  const uint32_t* Ap[2] = {A[0], A[1]};
+  const uint32_t* Sp[2] = {S[0], S[1]};
+  const uint8_t* Mp[2] = {m0, m1};
+  const uint64_t Lp[2] = {l0, l1};
+  uint32_t ok[2];
+  HostATab at;
+  if (mode == 0) verify_n<kStrict, 2>(ok, Ap, Sp, Mp, Lp, at, bcomb());
+  else verify_n<kCofactorless, 2>(ok, Ap, Sp, Mp, Lp, at, bcomb());
+  out2[0] = (int)ok[0];
+  out2[1] = (int)ok[1];
+}
+// The key-cache path (combs of -A_j) for two signatures.
+void nth_verify_cached_pair(int mode, const uint8_t* pk64, const uint8_t* sig128, const uint8_t* m0, uint64_t l0,
+                            const uint8_t* m1, uint64_t l1, int* out2) {
+  alignas(16) uint32_t A[2][8], S[2][16];
+  std::memcpy(A, pk64, 64);
+  std::memcpy(S, sig128, 128);
+  static HostWComb ca[2];
+  const unsigned long long cm = g_fe_mul, cs = g_fe_sq;  // key-cache build is not per signature
+  const uint32_t meta[2] = {key_comb(ca[0], A[0]), key_comb(ca[1], A[1])};
+  g_fe_mul = cm;
+  g_fe_sq = cs;
+  ca[0].memo.clear();
+  ca[1].memo.clear();
+  const uint32_t* Ap[2] = {A[0], A[1]};
+  const uint32_t* Sp[2] = {S[0], S[1]};
+  const uint8_t* Mp[2] = {m0, m1};
+  const uint64_t Lp[2] = {l0, l1};
+  uint32_t ok[2];
+  if (mode == 0) verify_cached_n<kStrict, 2>(ok, meta, Ap, Sp, Mp, Lp, ca, bcomb());
+  else verify_cached_n<kCofactorless, 2>(ok, meta, Ap, Sp, Mp, Lp, ca, bcomb());
+  out2[0] = (int)ok[0];
+  out2[1] = (int)ok[1];
 }
 void nth_sign(const uint8_t* seed, const uint8_t* msg, uint64_t len, uint8_t* pk, uint8_t* sig) {
   uint32_t sw[8], A[8], R[8], s[8];
   words(sw, seed);
-  sign_one(A, R, s, sw, msg, len, btab());
+  sign_one(A, R, s, sw, msg, len, bcomb());
   std::memcpy(pk, A, 32);
   std::memcpy(sig, R, 32);
   std::memcpy(sig + 32, s, 32);
 }
-void nth_counts_reset() { g_fe_mul = g_fe_sq = 0; btab(); g_fe_mul = g_fe_sq = 0; }
+// The device's wide-comb construction run on the host for one chunk: entries
+// j0-1 .. j0+63 (j0 = 1 + 64c; entry j0-1 only written for c = 0) of position
+// pos of the comb of P (negate: of -P), as 65 x 32 words.  Returns kKey* bits.
+uint32_t nth_wcomb_chunk(const uint8_t* enc32, int negate, int pos, int c, uint32_t* out) {
+  uint32_t w[8];
+  words(w, enc32);
+  ge_p3 P;
+  const uint32_t ok = ge_frombytes_w(P, w);
+  const uint32_t meta = (ok ? kKeyDecodes : 0u) | (ge_is_small_order(P) ? kKeySmallOrder : 0u);
+  if (!ok) ge_p3_0(P);
+  if (negate) {
+    fe_neg(P.X, P.X);
+    fe_carry(P.X);
+    fe_neg(P.T, P.T);
+    fe_carry(P.T);
+  }
+  static uint32_t bases[kWPos * 40];
+  wcomb_bases(bases, P);
+  static uint32_t tmp[kWChunk * 10];
+  std::memset(out, 0, 65 * kWStride * 4);
+  wcomb_fill(out + kWStride, tmp, bases + 40 * pos, (uint32_t)c);
+  return meta;
+}
+void nth_counts_reset() { bcomb(); g_fe_mul = g_fe_sq = 0; }
 unsigned long long nth_count_mul() { return g_fe_mul; }
 unsigned long long nth_count_sq() { return g_fe_sq; }
 }

@@ -2,7 +2,8 @@
 for the host by tests/cpp/).  These stress the radix-2^25.5 bound discipline at
 the extreme limb values the point formulas can produce (a silent u64 overflow
 would only show on adversarial limbs, never on random signatures), and replay
-the golden corpus through the same verify_one<> / sign_one the kernels run.
+the golden corpus through the same verify_n<> / verify_cached_n<> / sign_one the
+kernels run, and check the wide-comb construction against a textbook curve model.
 """
 import hashlib
 import json
@@ -94,6 +95,59 @@ def test_corpus_through_device_code():
         pk, sig, m = d["pk"][i].tobytes(), d["sig"][i].tobytes(), d["msg"][o:o + n].tobytes()
         assert H.verify(0, pk, sig, m) == bool(d["strict"][i]), i
         assert H.verify(1, pk, sig, m) == bool(d["batch_rule"][i]), i
+
+
+def test_corpus_pairs_through_device_code():
+    """The two-per-lane path (one shared inversion) the verify kernels run, and the
+    key-cache path; each corpus entry is paired with its neighbour."""
+    d = np.load(os.path.join(GOLD, "ed25519_corpus.npz"))
+    n = len(d["cat"])
+
+    def entry(i):
+        o, ln = int(d["off"][i]), int(d["len"][i])
+        return d["pk"][i].tobytes(), d["sig"][i].tobytes(), d["msg"][o:o + ln].tobytes()
+
+    for i in range(n):
+        j = (i + 1) % n
+        a, b = entry(i), entry(j)
+        for mode, key in ((0, "strict"), (1, "batch_rule")):
+            want = (bool(d[key][i]), bool(d[key][j]))
+            assert H.verify_pair(mode, *a, *b) == want, (i, mode)
+            if i % 3 == 0:
+                assert H.verify_pair(mode, *a, *b, cached=True) == want, (i, mode, "cached")
+
+
+def _model():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLD, "make_golden.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_wide_comb_construction_vs_model():
+    """wcomb_bases + wcomb_fill (the device build of j * 2^(16 i) * P, affine niels
+    with one batched inversion per chunk) against the textbook model."""
+    M = _model()
+    with open(os.path.join(GOLD, "fixtures_reference.json")) as f:
+        pk = bytes.fromhex(json.load(f)["keys"][1]["pk"])
+    cases = [(M.encode(M.BASE), 0, M.BASE), (pk, 1, M.pneg(M.decode(pk)))]
+    for enc, neg, pt in cases:
+        for pos in (0, 1, 15):
+            base = M.pmul(2 ** (16 * pos), pt)
+            for c in (0, 1, 511):
+                meta, e = H.wcomb_chunk(enc, neg, pos, c)
+                assert meta == 1
+                q = M.pmul(64 * c, base)
+                for idx in range(65):
+                    if idx or c == 0:
+                        X, Y, Z, _ = q
+                        zi = M.inv(Z)
+                        x, y = X * zi % M.P, Y * zi % M.P
+                        want = ((y + x) % M.P, (y - x) % M.P, 2 * M.D * x * y % M.P)
+                        got = tuple(H.value(e[idx][10 * k:10 * k + 10]) % M.P for k in range(3))
+                        assert got == want, (pos, c, idx)
+                    q = M.padd(q, base)
 
 
 def test_sign_fixture_through_device_code():
