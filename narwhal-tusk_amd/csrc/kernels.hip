@@ -192,8 +192,8 @@ __global__ __launch_bounds__(kBlock, OCC) void k_ed25519_verify(
 // Verification against a cached committee: two signatures per lane (wave w,
 // lane l: signatures 128w + l and 128w + 64 + l); key_idx[i] selects the key
 // (>= nkeys -> unknown key -> reject).
-template <int MODE>
-__global__ __launch_bounds__(kBlock, 2) void k_ed25519_verify_keyset(
+template <int MODE, int OCC>
+__global__ __launch_bounds__(kBlock, OCC) void k_ed25519_verify_keyset(
     const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
     const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t n,
     const uint32_t* __restrict__ meta, const uint32_t* __restrict__ enc, const uint32_t* __restrict__ combA,
@@ -306,24 +306,36 @@ hipError_t launch_sha512_trunc32(const uint8_t* d_data, const uint64_t* d_off, c
   return hipGetLastError();
 }
 
-// Occupancy variant of the verify kernel (waves per SIMD the register
-// allocator targets).  NT_VERIFY_OCC selects at run time (A/B measurement);
-// default 2.
+// Occupancy variants (waves per SIMD the register allocator targets), chosen
+// at run time for A/B measurement: NT_VERIFY_OCC in {1, 2, 3} (default 2),
+// NT_KEYSET_OCC in {2, 3} (default 3).
+static int env_occ(const char* name, int dflt, int lo, int hi) {
+  const char* e = std::getenv(name);
+  const int v = e ? std::atoi(e) : dflt;
+  return v < lo || v > hi ? dflt : v;
+}
 static int verify_occ() {
-  static int occ = [] {
-    const char* e = std::getenv("NT_VERIFY_OCC");
-    return (e && std::atoi(e) == 1) ? 1 : 2;
-  }();
+  static const int occ = env_occ("NT_VERIFY_OCC", 2, 1, 3);
   return occ;
 }
+static int keyset_occ() {
+  static const int occ = env_occ("NT_KEYSET_OCC", 3, 2, 3);
+  return occ;
+}
+int verify_occupancy() { return verify_occ(); }
 
 template <int MODE>
 static void launch_verify_mode(uint64_t blocks, const uint8_t* d_pk, const uint8_t* d_sig,
                                const uint8_t* d_msg, const uint64_t* d_off, const uint64_t* d_len,
                                uint64_t n, const uint32_t* d_combB, void* d_ws, uint64_t* d_out_words,
                                hipStream_t s) {
-  if (verify_occ() == 1)
+  const int occ = verify_occ();
+  if (occ == 1)
     hipLaunchKernelGGL((k_ed25519_verify<MODE, 1>), dim3((uint32_t)blocks), dim3(kBlock), 0, s,
+                       (const uint32_t*)d_pk, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_combB,
+                       (uint4*)d_ws, (unsigned long long*)d_out_words);
+  else if (occ == 3)
+    hipLaunchKernelGGL((k_ed25519_verify<MODE, 3>), dim3((uint32_t)blocks), dim3(kBlock), 0, s,
                        (const uint32_t*)d_pk, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_combB,
                        (uint4*)d_ws, (unsigned long long*)d_out_words);
   else
@@ -396,14 +408,19 @@ hipError_t launch_verify_keyset(int mode, const uint32_t* d_key_idx, const uint8
                                 const uint32_t* d_combB, uint64_t* d_out_words, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const uint64_t blocks = (n + 2 * kBlock - 1) / (2 * kBlock);  // two signatures per lane
-  if (mode == kStrict)
-    hipLaunchKernelGGL(k_ed25519_verify_keyset<kStrict>, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_key_idx,
-                       (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_meta, d_enc, d_combA, nkeys, d_combB,
-                       (unsigned long long*)d_out_words);
-  else
-    hipLaunchKernelGGL(k_ed25519_verify_keyset<kCofactorless>, dim3((uint32_t)blocks), dim3(kBlock), 0, s,
-                       d_key_idx, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_meta, d_enc, d_combA, nkeys,
-                       d_combB, (unsigned long long*)d_out_words);
+  const bool o3 = keyset_occ() == 3;
+#define NT_KS_LAUNCH(M, O)                                                                                   \
+  hipLaunchKernelGGL((k_ed25519_verify_keyset<M, O>), dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_key_idx, \
+                     (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_meta, d_enc, d_combA, nkeys, d_combB,  \
+                     (unsigned long long*)d_out_words)
+  if (mode == kStrict) {
+    if (o3) NT_KS_LAUNCH(kStrict, 3);
+    else NT_KS_LAUNCH(kStrict, 2);
+  } else {
+    if (o3) NT_KS_LAUNCH(kCofactorless, 3);
+    else NT_KS_LAUNCH(kCofactorless, 2);
+  }
+#undef NT_KS_LAUNCH
   return hipGetLastError();
 }
 

@@ -28,5 +28,6 @@ size_t wcomb_bytes_per_key();
 size_t wcomb_bases_bytes_per_key();
 size_t wcomb_fill_tmp_bytes_per_key();
 size_t ws_bytes_per_slot();
+int verify_occupancy();  // waves per SIMD of the selected verify kernel variant
 
 }  // namespace nt

@@ -112,8 +112,12 @@ struct Device {
       if (hipMalloc(&d_combB, nt::wcomb_bytes_per_key()) != hipSuccess) return NT_ENOMEM;
       NT_CHK0(build_wcombs(kB, 1, 0, d_combB, nullptr));
     }
-    // one workspace slot per resident workgroup; default 4 per CU
-    uint32_t slots = (uint32_t)prop.multiProcessorCount * 4;
+    // Workspace slots = grid cap of the verify kernel.  Four times the resident
+    // workgroups (256-thread blocks, `occupancy` waves per SIMD, 4 SIMDs per CU):
+    // up to 2M signatures per launch the grid is then one 512-signature block per
+    // slot and the hardware dispatcher balances the tail (interleaved A/B on
+    // MI355X, tools/ab_env.sh: ~1% over 1x and 2x resident).
+    uint32_t slots = (uint32_t)prop.multiProcessorCount * (uint32_t)nt::verify_occupancy() * 4;
     if (const char* e = std::getenv("NT_WS_SLOTS")) slots = (uint32_t)std::max(1, std::atoi(e));
     ws_slots = slots;
     sign_blocks = (uint32_t)prop.multiProcessorCount * 8;
