@@ -181,28 +181,32 @@ NT_HD NT_INLINE void wcomb_fill(uint32_t* dst, uint32_t* tmp, const uint32_t* ba
 }
 
 // ---------------------------------------------------------------------------
-// Variable-base part: [k](-A) with 4-bit signed windows over a per-lane table
+// Variable-base part: [u](+-A) + [v](-R) with joint 4-bit signed windows
+// over two per-lane tables (entries 0..8: j*(+-A), 9..17: j*(-R))
 // ---------------------------------------------------------------------------
+constexpr uint32_t kTabR = 9;  // first entry of the R table
 
-// Decode A (dalek decompress), strict: reject small order; store j * (-A), j = 0..8.
-template <int MODE, class ATab>
-NT_HD NT_INLINE uint32_t atab_build(const uint32_t Aw[8], ATab& at) {
-  ge_p3 A;
-  uint32_t ok = ge_frombytes_w(A, Aw);
-  if (MODE == kStrict) ok &= ge_is_small_order(A) ^ 1u;
-  ge_p3 An;
-  fe_neg(An.X, A.X);
-  fe_carry(An.X);
-  An.Y = A.Y;
-  An.Z = A.Z;
-  fe_neg(An.T, A.T);
-  fe_carry(An.T);
+// store j * (neg ? -P : P), j = 0..8, at entries e0 .. e0+8
+template <class ATab>
+NT_HD NT_INLINE void ptab_build(const ge_p3& P, uint32_t neg, ATab& at, uint32_t e0) {
+  ge_p3 Q;
+  fe n;
+  fe_neg(n, P.X);
+  fe_carry(n);
+  fe_cmov(n, P.X, neg ^ 1u);
+  Q.X = n;
+  fe_neg(n, P.T);
+  fe_carry(n);
+  fe_cmov(n, P.T, neg ^ 1u);
+  Q.T = n;
+  Q.Y = P.Y;
+  Q.Z = P.Z;
   ge_cached c0, c1;
   ge_cached_0(c0);
-  at.store(0, c0);
-  ge_p3_to_cached(c1, An);
-  at.store(1, c1);
-  ge_p3 cur = An;
+  at.store(e0, c0);
+  ge_p3_to_cached(c1, Q);
+  at.store(e0 + 1, c1);
+  ge_p3 cur = Q;
 #pragma unroll 1
   for (uint32_t j = 2; j < 9; ++j) {
     ge_cp t;
@@ -210,21 +214,46 @@ NT_HD NT_INLINE uint32_t atab_build(const uint32_t Aw[8], ATab& at) {
     ge_cp_to_p3(cur, t);
     ge_cached cj;
     ge_p3_to_cached(cj, cur);
-    at.store(j, cj);
+    at.store(e0 + j, cj);
   }
-  return ok;
 }
 
-// t = [k](-A) (completed) for k < 2^253 given as 64 signed 4-bit digits.
-// The top digit seeds the accumulator (no doublings of the identity): 252
-// doublings and 63 additions.  Every lane follows the same schedule.
-template <class ATab>
-NT_HD NT_INLINE void ladder_a(ge_cp& t, const uint32_t kd[8], const ATab& at) {
-  uint32_t kw[8];
+// wave-uniform maximum: every lane of a wave then runs the same window count
+NT_HD NT_INLINE int wave_max(int x) {
+#if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
-  for (int i = 0; i < 8; ++i) kw[i] = kd[i];
+  for (int o = 32; o > 0; o >>= 1) {
+    const int y = __shfl_xor(x, o);
+    x = x > y ? x : y;
+  }
+  return __builtin_amdgcn_readfirstlane(x);
+#else
+  return x;
+#endif
+}
+
+// signed 4-bit digit wi of a sc_recode_w4 string (wi wave-uniform)
+NT_HD NT_INLINE int32_t w4_digit(const uint32_t d[8], int wi) {
+  return (int32_t)(((pick<8>(d, wi >> 3) >> (4 * (wi & 7))) & 15u) ^ 8u) - 8;
+}
+
+// acc (completed -> p3) + table entry e0 + |d| with the sign of d
+template <class ATab>
+NT_HD NT_INLINE void ladder_add(ge_cp& t, int32_t d, uint32_t e0, const ATab& at) {
+  ge_cached ce;
+  at.load(e0 + (uint32_t)(d < 0 ? -d : d), ce);  // latency overlaps the conversion
+  ge_p3 u;
+  ge_cp_to_p3(u, t);
+  ge_cached_cneg(ce, d < 0);
+  ge_add_cached(t, u, ce);
+}
+
+// t = [u](+-A) + [v](-R) (completed) for W-window digit strings ud, vd:
+// 4(W-1) doublings and 2W - 1 additions.  The top A digit seeds the accumulator.
+template <class ATab>
+NT_HD NT_INLINE void ladder_ar(ge_cp& t, const uint32_t ud[8], const uint32_t vd[8], int W, const ATab& at) {
   {
-    const int32_t d = (int32_t)((kw[7] >> 28) ^ 8u) - 8;
+    const int32_t d = w4_digit(ud, W - 1);
     ge_cached ce;
     at.load((uint32_t)(d < 0 ? -d : d), ce);
     ge_cached_cneg(ce, d < 0);
@@ -235,27 +264,17 @@ NT_HD NT_INLINE void ladder_a(ge_cp& t, const uint32_t kd[8], const ATab& at) {
     fe_carry(t.Y);
     t.Z = ce.Z2;
     t.T = ce.Z2;
+    ladder_add(t, w4_digit(vd, W - 1), kTabR, at);
   }
 #pragma unroll 1
-  for (int wi = 7; wi >= 0; --wi) {
-    const uint32_t cur = kw[7];
-#pragma unroll
-    for (int m = 7; m > 0; --m) kw[m] = kw[m - 1];
+  for (int wi = W - 2; wi >= 0; --wi) {
+    ge_p2 acc;
+    ge_cp_to_p2(acc, t);
 #pragma unroll 1
-    for (int j = (wi == 7 ? 6 : 7); j >= 0; --j) {
-      ge_p2 acc;
-      ge_cp_to_p2(acc, t);
-#pragma unroll 1
-      for (int r = 0; r < 3; ++r) ge_dbl_p2(acc, acc);
-      ge_dbl(t, acc);
-      const int32_t dk = (int32_t)(((cur >> (4 * j)) & 15u) ^ 8u) - 8;
-      ge_cached ce;
-      at.load((uint32_t)(dk < 0 ? -dk : dk), ce);  // latency overlaps the conversion
-      ge_p3 u;
-      ge_cp_to_p3(u, t);
-      ge_cached_cneg(ce, dk < 0);
-      ge_add_cached(t, u, ce);
-    }
+    for (int r = 0; r < 3; ++r) ge_dbl_p2(acc, acc);
+    ge_dbl(t, acc);
+    ladder_add(t, w4_digit(ud, wi), 0, at);
+    ladder_add(t, w4_digit(vd, wi), kTabR, at);
   }
 }
 
@@ -325,42 +344,64 @@ NT_HD NT_INLINE void finish_compare(uint32_t ok[N], const ge_p2 P[N], const uint
   }
 }
 
-// N (1 or 2) verifications per lane.  A[j] = 8 pk words, sig[j] = 16 words
-// (R || s), msg[j]/len[j] = message.  at is this lane's j*(-A) table (reused
-// by the N signatures in turn), wb the wide comb of B.
+// One verification (A, R, s encodings as words), half-size scalars:
+//   ok  <=>  s < L, A and R decode, (strict) neither is small order, and
+//            [v s mod L]B - [u]A - [v]R == identity     (= [v]([s]B - [k]A - R))
+// with (u, v) = sc_halfsize(k), k = SHA-512(R || A || M) mod L.  at holds this
+// lane's tables, wb is the wide comb of B.
+template <int MODE, class ATab, class WComb>
+NT_HD NT_INLINE uint32_t verify_one(const uint32_t Aw[8], const uint32_t Rw[8], const uint32_t Sw[8],
+                                    const uint8_t* msg, uint64_t len, ATab& at, const WComb& wb) {
+  uint32_t ok = sc_is_canonical(Sw);
+  uint32_t u[8], v[8], uneg;
+  int bits;
+  {
+    uint32_t k[8];
+    hram_scalar(k, Rw, Aw, msg, len);
+    bits = sc_halfsize(u, uneg, v, k);
+  }
+  {
+    ge_p3 A;
+    ok &= ge_frombytes_w(A, Aw);
+    if (MODE == kStrict) ok &= ge_is_small_order(A) ^ 1u;
+    ptab_build(A, uneg ^ 1u, at, 0);  // -[u]A = [|u|](u < 0 ? A : -A)
+  }
+  {
+    ge_p3 R;
+    ok &= ge_frombytes_w(R, Rw);
+    if (MODE == kStrict) ok &= ge_is_small_order(R) ^ 1u;
+    ptab_build(R, 1u, at, kTabR);
+  }
+  uint32_t w[8], ud[8], vd[8];
+  sc_mul(w, v, Sw);
+  sc_recode_w4(ud, u);
+  sc_recode_w4(vd, v);
+  const int W = wave_max((bits + 5) >> 2);  // 4W >= bits + 2: the signed top digit absorbs the carry
+  ge_cp t;
+  ladder_ar(t, ud, vd, W, at);
+  ge_p3 acc;
+  ge_cp_to_p3(acc, t);
+  wcomb_acc(acc, w, wb);
+  return ok & fe_iszero(acc.X) & fe_eq(acc.Y, acc.Z);
+}
+
+// N verifications per lane in turn.  A[j] = 8 pk words, sig[j] = 16 words
+// (R || s), msg[j]/len[j] = message; at is this lane's table storage.
 template <int MODE, int N, class ATab, class WComb>
 NT_HD NT_INLINE void verify_n(uint32_t ok[N], const uint32_t* const A[N], const uint32_t* const sig[N],
                               const uint8_t* const msg[N], const uint64_t len[N], ATab& at, const WComb& wb) {
-  ge_p2 P[N];
 #pragma unroll 1
   for (int j = 0; j < N; ++j) {
     const uint32_t* sj = pick<N>(sig, j);
-    uint32_t Aw[8], Sw[8], kd[8];
+    uint32_t Aw[8], Rw[8], Sw[8];
     ld8(Aw, pick<N>(A, j));
+    ld8(Rw, sj);
     ld8(Sw, sj + 8);
-    uint32_t okj = sc_is_canonical(Sw);
-    okj &= atab_build<MODE>(Aw, at);
-    {
-      uint32_t Rw[8], k[8];
-      ld8(Rw, sj);
-      hram_scalar(k, Rw, Aw, pick<N>(msg, j), pick<N>(len, j));
-      sc_recode_w4(kd, k);
-    }
-    ge_cp t;
-    ladder_a(t, kd, at);
-    ge_p3 acc;
-    ge_cp_to_p3(acc, t);
-    wcomb_acc(acc, Sw, wb);
-    // keep the first result in registers (select, not a dynamically indexed array)
+    const uint32_t okj = verify_one<MODE>(Aw, Rw, Sw, pick<N>(msg, j), pick<N>(len, j), at, wb);
 #pragma unroll
-    for (int q = 0; q < N; ++q) {
-      if (q == j) {
-        ge_p3_to_p2(P[q], acc);
-        ok[q] = okj;
-      }
-    }
+    for (int q = 0; q < N; ++q)
+      if (q == j) ok[q] = okj;
   }
-  finish_compare<MODE, N>(ok, P, sig);
 }
 
 // Key-cache variant: ca[j] is the wide comb of -A_j, meta[j] its kKey* bits.

@@ -29,7 +29,7 @@
 namespace nt {
 
 constexpr int kBlock = 256;
-constexpr int kAEntries = 9;          // |digit| in 0..8
+constexpr int kAEntries = 18;         // j*(+-A) and j*(-R), |digit| in 0..8
 constexpr int kAQuads = 10;           // uint4 per cached entry (40 words)
 
 // --------------------------------------------------------------------------

@@ -6,6 +6,8 @@
 //   Scalar::from_hash      -> sc_reduce512 of the 64-byte SHA-512 output
 //   check_scalar (s decode) -> sc_is_canonical: accept iff s < L
 #pragma once
+#include <math.h>
+
 #include "constants.hpp"
 #include "nt_common.hpp"
 
@@ -160,6 +162,185 @@ NT_HD NT_INLINE void sc_recode_w16(uint32_t out[8], const uint32_t s[8]) {
     const uint32_t dhi = (hi - (carry << 16)) & 0xffffu;
     out[w] = dlo | (dhi << 16);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Half-size scalars (lattice reduction in dimension 2 over Z / 8L).
+//
+// For k < L find (u, v), v odd and 0 < v < L, with u == v k (mod 8L) and
+// |u|, v ~ 2^128.  Then for any points A, R of the curve (order | 8L) and any s:
+//      [v]([s]B - [k]A - R) = [v s mod L]B - [u]A - [v]R
+// and, because gcd(v, 8L) = 1, the left side is the identity iff
+// [s]B - [k]A - R is.  This turns the 253-bit variable-base scalar into two
+// ~128-bit ones (half the doublings) with EXACTLY the verdict of the
+// full-size equation -- for every A and R, torsion components included (the
+// lattice is taken mod 8L, not mod L, for that reason).
+//
+// Method: the extended Euclidean remainder sequence of (8L, k) (r_i == t_i k)
+// stopped at the first r < 2^127.5 (then |t| <= 8L / r_prev < 2^127.5).
+// Quotients are estimated from fp64 images of the remainders and rounded
+// DOWN (a short quotient is just a partial step), so every basis the loop
+// visits is an exact lattice basis with r0 |t1| + r1 |t0| = 8L and t0, t1 of
+// opposite signs; the result is therefore valid whatever the rounding.  If
+// the last t is even, the odd one of the two neighbouring vectors with fewer
+// bits is used.  Anything unexpected (step cap, > 250 bits) falls back to the
+// trivial vector (k, 1).  Returns max(bitlen|u|, bitlen v) (never an
+// underestimate).  Per-lane loop lengths differ (~73 steps on average).
+// ---------------------------------------------------------------------------
+template <int N>
+NT_HD NT_INLINE double bn_to_f64(const uint32_t* a) {
+  double d = (double)a[N - 1];
+#pragma unroll
+  for (int i = N - 2; i >= 0; --i) d = fma(d, 4294967296.0, (double)a[i]);
+  return d;
+}
+
+// bit length of a non-negative integer from its fp64 image (rounding can only
+// overestimate by one)
+NT_HD NT_INLINE int f64_bitlen(double d) {
+  int e;
+  frexp(d, &e);
+  return d == 0.0 ? 0 : e;
+}
+
+// a < b over N words
+template <int N>
+NT_HD NT_INLINE uint32_t bn_lt(const uint32_t* a, const uint32_t* b) {
+  uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) br = ((uint64_t)a[i] - b[i] - br) >> 63;
+  return (uint32_t)br;
+}
+
+// a -= q b over N words (caller guarantees no underflow)
+template <int N>
+NT_HD NT_INLINE void bn_submul1(uint32_t* a, const uint32_t* b, uint32_t q) {
+  uint64_t c = 0;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint64_t p = (uint64_t)q * b[i] + c;
+    c = p >> 32;
+    const uint64_t t = (uint64_t)a[i] - (uint32_t)p - br;
+    a[i] = (uint32_t)t;
+    br = (uint32_t)(t >> 63);
+  }
+}
+
+// a += q b over N words (caller guarantees no overflow)
+template <int N>
+NT_HD NT_INLINE void bn_addmul1(uint32_t* a, const uint32_t* b, uint32_t q) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint64_t p = (uint64_t)q * b[i] + a[i] + c;
+    a[i] = (uint32_t)p;
+    c = p >> 32;
+  }
+}
+
+// floor(d0 / d1) rounded down by a 2^-40 margin, clamped to [1, 2^32 - 1]
+NT_HD NT_INLINE uint32_t lat_quot(double d0, double d1) {
+  const double qd = d0 / d1 * (1.0 - 0x1p-40);
+  return qd >= 4294967295.0 ? 0xffffffffu : (qd < 1.0 ? 1u : (uint32_t)qd);
+}
+
+constexpr int kLatMaxSteps = 600;
+constexpr double kLatStop = 0x1.6a09e667f3bcdp+127;  // 2^127.5
+
+NT_HD NT_INLINE int sc_halfsize(uint32_t u[8], uint32_t& uneg, uint32_t v[8], const uint32_t k[8]) {
+  uint32_t r0[8], r1[8], t0[4], t1[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    r0[i] = kSc8L[i];
+    r1[i] = k[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) t0[i] = t1[i] = 0;
+  t1[0] = 1;
+  uint32_t t1neg = 0;
+  double d0 = bn_to_f64<8>(r0), d1 = bn_to_f64<8>(r1);
+  int steps = 0;
+  // Inside the loop r1 >= 2^127.5, so |t0|, |t1| <= 8L / r1 < 2^128: 4 words.
+  while (d1 >= kLatStop && steps < kLatMaxSteps) {
+    const uint32_t q = lat_quot(d0, d1);
+    bn_submul1<8>(r0, r1, q);
+    bn_addmul1<4>(t0, t1, q);
+    d0 = bn_to_f64<8>(r0);
+    const uint32_t sw = bn_lt<8>(r0, r1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t a = r0[i], b = r1[i];
+      r0[i] = sw ? b : a;
+      r1[i] = sw ? a : b;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t a = t0[i], b = t1[i];
+      t0[i] = sw ? b : a;
+      t1[i] = sw ? a : b;
+    }
+    const double e0 = d0;
+    d0 = sw ? d1 : d0;
+    d1 = sw ? e0 : d1;
+    t1neg ^= sw;
+    ++steps;
+  }
+  int bits;
+  if (t1[0] & 1u) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      u[i] = r1[i];
+      v[i] = i < 4 ? t1[i] : 0u;
+    }
+    uneg = t1neg;
+    bits = f64_bitlen(d1);
+    const int bt = f64_bitlen(bn_to_f64<4>(t1));
+    bits = bt > bits ? bt : bits;
+  } else {
+    // t1 even => t0 odd (gcd(t0, t1) = 1).  Candidates with the sign of t0:
+    // b0 = (r0, t0) and b2 = b0 - q b1 = (r0 - q r1, |t0| + q |t1|).
+    uint32_t r2[8], t2[8], t1w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      r2[i] = r0[i];
+      t2[i] = i < 4 ? t0[i] : 0u;
+      t1w[i] = i < 4 ? t1[i] : 0u;
+    }
+    const uint32_t q = d1 > 0.0 ? lat_quot(d0, d1) : 1u;
+    if (d1 > 0.0) bn_submul1<8>(r2, r1, q);
+    bn_addmul1<8>(t2, t1w, q);
+    const int b0r = f64_bitlen(d0), b0t = f64_bitlen(bn_to_f64<4>(t0));
+    const int b2r = f64_bitlen(bn_to_f64<8>(r2)), b2t = f64_bitlen(bn_to_f64<8>(t2));
+    const int c0 = b0r > b0t ? b0r : b0t;
+    const int c2 = b2r > b2t ? b2r : b2t;
+    const bool use2 = d1 > 0.0 && c2 < c0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      u[i] = use2 ? r2[i] : r0[i];
+      v[i] = use2 ? t2[i] : (i < 4 ? t0[i] : 0u);
+    }
+    uneg = t1neg ^ 1u;
+    bits = use2 ? c2 : c0;
+  }
+  if (steps >= kLatMaxSteps || bits > 250) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      u[i] = k[i];
+      v[i] = 0;
+    }
+    v[0] = 1;
+    uneg = 0;
+    bits = 253;
+  }
+  return bits;
+}
+
+// (v * s) mod L for v, s < 2^256
+NT_HD NT_INLINE void sc_mul(uint32_t out[8], const uint32_t a[8], const uint32_t b[8]) {
+  uint32_t p[16];
+  bn_mul<8, 8>(p, a, b);
+  sc_reduce512(out, p);
 }
 
 }  // namespace nt

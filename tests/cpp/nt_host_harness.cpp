@@ -21,7 +21,7 @@ using namespace nt;
 
 namespace {
 struct HostATab {
-  ge_cached e[9];
+  ge_cached e[18];
   void store(uint32_t j, const ge_cached& c) { e[j] = c; }
   void load(uint32_t j, ge_cached& c) const { c = e[j]; }
 };
