@@ -254,7 +254,7 @@ def bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_r
     return {"value": round(gbs, 2), "unit": "GB/s (message bytes)", "workload": "cfg4: %d x %d B" % (m_total, ml),
             "ms_per_step": round(wall * 1e3 / steps, 3), "kernel_ms": round(kms, 3),
             "hbm_frac": round((m * padded / (kms * 1e-3)) / 1e9 / HBM_PEAK_GBS, 4),
-            "note": "one lane per message: 16,384 lanes = 256 waves, latency-bound (SURVEY H2)",
+            "note": "k_sha512_pipe: per 64 messages a producer wave expands K+W into LDS, a consumer wave runs the rounds; bound by the consumer wave's serial per-block stream (latency-bound, SURVEY H2), not HBM",
             "spot_check_ok": bool(ok)}
 
 

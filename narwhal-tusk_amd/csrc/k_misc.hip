@@ -1,4 +1,6 @@
-// kernels.hip -- gfx950 kernels of the Narwhal/Tusk crypto hot path.
+// k_misc.hip -- gfx950 kernels of the Narwhal/Tusk crypto hot path other than
+// verification (which lives in k_verify_*.hip / k_keyset_*.hip), plus every
+// host launcher.  Kernel map of the library:
 //
 //   k_sha512_trunc32      one lane per message, Digest = SHA-512[..32]
 //                         (worker/src/processor.rs:38; primary/src/messages.rs:70-84,145-153,226-234)
@@ -19,18 +21,9 @@
 // addition); [k](-A) uses 4-bit windows over a per-lane 9-entry cached table in
 // a global workspace laid out lane-minor so each lane's 16-byte accesses
 // coalesce across the workgroup.
-#include <hip/hip_runtime.h>
-
-#include <cstdlib>
-
-#include "ed25519_ops.hpp"
-#include "kernels.hpp"
+#include "kernels_common.hpp"
 
 namespace nt {
-
-constexpr int kBlock = 256;
-constexpr int kAEntries = 18;         // j*(+-A) and j*(-R), |digit| in 0..8
-constexpr int kAQuads = 10;           // uint4 per cached entry (40 words)
 
 // --------------------------------------------------------------------------
 // SHA-512 digests
@@ -50,64 +43,104 @@ __global__ __launch_bounds__(kBlock) void k_sha512_trunc32(const uint8_t* __rest
   o[1] = make_uint4(w[4], w[5], w[6], w[7]);
 }
 
-// --------------------------------------------------------------------------
-// Table accessors
-// --------------------------------------------------------------------------
-// Wide comb of one point, layout [pos][entry][32 words]; 8 x 16-byte loads.
-struct WideComb {
-  const uint32_t* base;
-  NT_D NT_INLINE void load(uint32_t pos, uint32_t idx, ge_niels& q) const {
-    const uint4* e = (const uint4*)(base + ((size_t)pos * kWEntries + idx) * kWStride);
-    uint32_t w[32];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint4 v = e[i];
-      w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
-    }
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      q.ypx.v[i] = w[i];
-      q.ymx.v[i] = w[10 + i];
-      q.xy2d.v[i] = w[20 + i];
-    }
+// Few long messages (n <= kPipeMaxMsgs, e.g. config 4: 16,384 x 500 kB): one
+// lane per message is latency-bound (the per-block instruction stream of a
+// wave alone on its SIMD), so the work of a block is split over two waves of
+// a 128-thread workgroup that hold the same 64 messages.  Wave 0 (producer)
+// loads block b and expands K[t] + W[t], t < 80, into an LDS ring slot; wave 1
+// (consumer) runs the 80 rounds of block b-1 from the other slot.  One
+// s_barrier per block; the consumer's stream is ~2/3 of the one-wave stream.
+constexpr int kPipeMaxMsgs = 32768;  // 80 KB LDS per workgroup: 2 per CU
+struct KwLdsSink {
+  uint4* slot;  // [40][64]
+  uint32_t lane;
+  template <int P>
+  NT_D NT_INLINE void put(uint64_t kw0, uint64_t kw1) {
+    slot[P * 64 + lane] = make_uint4((uint32_t)kw0, (uint32_t)(kw0 >> 32), (uint32_t)kw1, (uint32_t)(kw1 >> 32));
+  }
+};
+struct KwLdsSource {
+  const uint4* slot;
+  uint32_t lane;
+  template <int P>
+  NT_D NT_INLINE void get(uint64_t& kw0, uint64_t& kw1) const {
+    const uint4 q = slot[P * 64 + lane];
+    kw0 = ((uint64_t)q.y << 32) | q.x;
+    kw1 = ((uint64_t)q.w << 32) | q.z;
   }
 };
 
-constexpr size_t kWWordsPerKey = (size_t)kWPos * kWEntries * kWStride;
-
-// j*(-A) entries in the global workspace, layout [slot][entry][quad][lane] of
-// uint4: a lane's 16-byte accesses are adjacent to its neighbours'.
-struct WsATab {
-  uint4* ws;
-  uint32_t slot;
-  NT_D NT_INLINE uint4* at(uint32_t entry) const {
-    return ws + ((size_t)(slot * kAEntries + entry) * kAQuads) * kBlock + threadIdx.x;
+__global__ __launch_bounds__(128) void k_sha512_pipe(const uint8_t* __restrict__ data,
+                                                     const uint64_t* __restrict__ off,
+                                                     const uint64_t* __restrict__ len, uint64_t n,
+                                                     uint32_t* __restrict__ out) {
+  __shared__ uint4 ring[2][40 * 64];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint64_t gi = (uint64_t)blockIdx.x * 64 + lane;
+  const bool act = gi < n;
+  const uint64_t i = act ? gi : n - 1;
+  const uint8_t* msg = data + off[i];
+  const uint64_t ln = len[i];
+  const uint64_t nblocks = (ln + 17 + 127) / 128;
+  const uint64_t nfull = ln / 128;
+  // trip count shared by both waves (same 64 messages): max over the lanes
+  uint32_t nb = (uint32_t)nblocks;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t y = __shfl_xor(nb, o);
+    nb = nb > y ? nb : y;
   }
-  NT_D NT_INLINE void store(uint32_t entry, const ge_cached& c) const {
-    uint32_t w[40];
+  nb = __builtin_amdgcn_readfirstlane(nb);
+  if (wave == 0) {
+    // full blocks are prefetched one block ahead (HBM latency ~ half a block's work)
+    uint32_t pre[32];
+    if (nfull > 0) load_words<32>(pre, msg);
+#pragma unroll 1
+    for (uint32_t it = 0; it <= nb; ++it) {
+      if (it < nb) {
+        uint32_t blk[32];
+        if (it < nfull) {
 #pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      w[i] = c.YpX.v[i]; w[10 + i] = c.YmX.v[i]; w[20 + i] = c.Z2.v[i]; w[30 + i] = c.T2d.v[i];
+          for (int q = 0; q < 32; ++q) blk[q] = pre[q];
+          if (it + 1 < nfull) load_words<32>(pre, msg + 128 * (uint64_t)(it + 1));
+        } else {
+          sha512_tail_block<0>(blk, nullptr, msg, ln, it, it + 1 == nblocks);
+        }
+        uint64_t W[16];
+        sha512_block_w(W, blk);
+        KwLdsSink sink{ring[it & 1], lane};
+        sha_kw_pairs<0>(W, sink);
+      }
+      __syncthreads();
     }
-    uint4* base = at(entry);
+  } else {
+    uint64_t st[8];
+    sha512_init(st);
+#pragma unroll 1
+    for (uint32_t it = 0; it <= nb; ++it) {
+      if (it > 0) {
+        const uint32_t b = it - 1;
+        uint64_t v[8];
 #pragma unroll
-    for (int q = 0; q < kAQuads; ++q)
-      base[(size_t)q * kBlock] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+        for (int q = 0; q < 8; ++q) v[q] = st[q];
+        const KwLdsSource src{ring[b & 1], lane};
+        sha_rounds_kw<0>(v, src);
+        const bool upd = b < nblocks;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) st[q] = upd ? add64(st[q], v[q]) : st[q];
+      }
+      __syncthreads();
+    }
+    if (act) {
+      uint32_t w[8];
+      sha512_out_words(w, st, 8);
+      uint4* o = (uint4*)(out + 8 * gi);
+      o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+      o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    }
   }
-  NT_D NT_INLINE void load(uint32_t entry, ge_cached& c) const {
-    uint32_t w[40];
-    const uint4* base = at(entry);
-#pragma unroll
-    for (int q = 0; q < kAQuads; ++q) {
-      const uint4 v = base[(size_t)q * kBlock];
-      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
-    }
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      c.YpX.v[i] = w[i]; c.YmX.v[i] = w[10 + i]; c.Z2.v[i] = w[20 + i]; c.T2d.v[i] = w[30 + i];
-    }
-  }
-};
+}
 
 // --------------------------------------------------------------------------
 // Wide-comb construction
@@ -146,90 +179,6 @@ __global__ void k_wcomb_fill(const uint32_t* __restrict__ bases, uint32_t nkeys,
   const uint32_t c = (uint32_t)(t % kWChunks);
   uint32_t* dst = comb + key * kWWordsPerKey + ((size_t)pos * kWEntries + 1 + (size_t)kWChunk * c) * kWStride;
   wcomb_fill(dst, tmp + t * (kWChunk * 10), bases + ((size_t)key * kWPos + pos) * 40, c);
-}
-
-// --------------------------------------------------------------------------
-// Verification: two signatures per lane, grid-stride over workspace slots.
-// Block iteration covers 512 signatures; wave w, lane l, slot j handles
-// signature base + 128 w + 64 j + l (so each verdict word is one ballot).
-// --------------------------------------------------------------------------
-template <int MODE, int OCC>
-__global__ __launch_bounds__(kBlock, OCC) void k_ed25519_verify(
-    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
-    const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t n,
-    const uint32_t* __restrict__ combB, uint4* __restrict__ ws, unsigned long long* __restrict__ out_bits) {
-  WsATab at{ws, blockIdx.x};
-  const WideComb wb{combB};
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t wofs = 128 * (uint64_t)(threadIdx.x >> 6);
-  for (uint64_t base = (uint64_t)blockIdx.x * 2 * kBlock; base < n; base += (uint64_t)gridDim.x * 2 * kBlock) {
-    uint32_t act[2];
-    const uint32_t* A[2];
-    const uint32_t* S[2];
-    const uint8_t* M[2];
-    uint64_t L[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const uint64_t gi = base + wofs + 64 * j + lane;
-      act[j] = gi < n;
-      const uint64_t i = act[j] ? gi : n - 1;
-      A[j] = pk + 8 * i;
-      S[j] = sig + 16 * i;
-      M[j] = msg + off[i];
-      L[j] = len[i];
-    }
-    uint32_t ok[2];
-    verify_n<MODE, 2>(ok, A, S, M, L, at, wb);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const unsigned long long bal = __ballot(ok[j] & act[j]);
-      const uint64_t wbase = base + wofs + 64 * j;
-      if (lane == 0 && wbase < n) out_bits[wbase >> 6] = bal;
-    }
-  }
-}
-
-// Verification against a cached committee: two signatures per lane (wave w,
-// lane l: signatures 128w + l and 128w + 64 + l); key_idx[i] selects the key
-// (>= nkeys -> unknown key -> reject).
-template <int MODE, int OCC>
-__global__ __launch_bounds__(kBlock, OCC) void k_ed25519_verify_keyset(
-    const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ sig, const uint8_t* __restrict__ msg,
-    const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t n,
-    const uint32_t* __restrict__ meta, const uint32_t* __restrict__ enc, const uint32_t* __restrict__ combA,
-    uint32_t nkeys, const uint32_t* __restrict__ combB, unsigned long long* __restrict__ out_bits) {
-  const uint64_t wave = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-  const uint32_t lane = threadIdx.x & 63u;
-  uint32_t act[2], m[2];
-  const uint32_t* A[2];
-  const uint32_t* S[2];
-  const uint8_t* M[2];
-  uint64_t L[2];
-  WideComb ca[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const uint64_t gi = 128 * wave + 64 * j + lane;
-    act[j] = gi < n;
-    const uint64_t i = act[j] ? gi : n - 1;
-    const uint32_t kraw = key_idx[i];
-    const uint32_t known = kraw < nkeys;
-    const uint32_t key = known ? kraw : 0u;
-    A[j] = enc + 8 * key;
-    S[j] = sig + 16 * i;
-    m[j] = known ? meta[key] : 0u;
-    M[j] = msg + off[i];
-    L[j] = len[i];
-    ca[j] = WideComb{combA + key * kWWordsPerKey};
-  }
-  const WideComb cb{combB};
-  uint32_t ok[2];
-  verify_cached_n<MODE, 2>(ok, m, A, S, M, L, ca, cb);
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const unsigned long long bal = __ballot(ok[j] & act[j]);
-    const uint64_t wbase = 128 * wave + 64 * j;
-    if (lane == 0 && wbase < n) out_bits[wbase >> 6] = bal;
-  }
 }
 
 // --------------------------------------------------------------------------
@@ -300,20 +249,17 @@ __global__ __launch_bounds__(kBlock) void k_ed25519_sign(const uint32_t* __restr
 hipError_t launch_sha512_trunc32(const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
                                  uint64_t n, uint8_t* d_out32, hipStream_t s) {
   if (n == 0) return hipSuccess;
+  if (n <= (uint64_t)kPipeMaxMsgs && !std::getenv("NT_SHA_NO_PIPE")) {
+    hipLaunchKernelGGL(k_sha512_pipe, dim3((uint32_t)((n + 63) / 64)), dim3(128), 0, s, d_data, d_off, d_len, n,
+                       (uint32_t*)d_out32);
+    return hipGetLastError();
+  }
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_sha512_trunc32, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_data, d_off,
                      d_len, n, (uint32_t*)d_out32);
   return hipGetLastError();
 }
 
-// Occupancy variants (waves per SIMD the register allocator targets), chosen
-// at run time for A/B measurement: NT_VERIFY_OCC in {1, 2, 3} (default 2),
-// NT_KEYSET_OCC in {2, 3} (default 3).
-static int env_occ(const char* name, int dflt, int lo, int hi) {
-  const char* e = std::getenv(name);
-  const int v = e ? std::atoi(e) : dflt;
-  return v < lo || v > hi ? dflt : v;
-}
 static int verify_occ() {
   static const int occ = env_occ("NT_VERIFY_OCC", 2, 1, 3);
   return occ;
@@ -323,26 +269,7 @@ static int keyset_occ() {
   return occ;
 }
 int verify_occupancy() { return verify_occ(); }
-
-template <int MODE>
-static void launch_verify_mode(uint64_t blocks, const uint8_t* d_pk, const uint8_t* d_sig,
-                               const uint8_t* d_msg, const uint64_t* d_off, const uint64_t* d_len,
-                               uint64_t n, const uint32_t* d_combB, void* d_ws, uint64_t* d_out_words,
-                               hipStream_t s) {
-  const int occ = verify_occ();
-  if (occ == 1)
-    hipLaunchKernelGGL((k_ed25519_verify<MODE, 1>), dim3((uint32_t)blocks), dim3(kBlock), 0, s,
-                       (const uint32_t*)d_pk, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_combB,
-                       (uint4*)d_ws, (unsigned long long*)d_out_words);
-  else if (occ == 3)
-    hipLaunchKernelGGL((k_ed25519_verify<MODE, 3>), dim3((uint32_t)blocks), dim3(kBlock), 0, s,
-                       (const uint32_t*)d_pk, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_combB,
-                       (uint4*)d_ws, (unsigned long long*)d_out_words);
-  else
-    hipLaunchKernelGGL((k_ed25519_verify<MODE, 2>), dim3((uint32_t)blocks), dim3(kBlock), 0, s,
-                       (const uint32_t*)d_pk, (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_combB,
-                       (uint4*)d_ws, (unsigned long long*)d_out_words);
-}
+int keyset_occupancy() { return keyset_occ(); }
 
 hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
                          const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
@@ -351,12 +278,10 @@ hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, co
   if (n == 0) return hipSuccess;
   uint64_t blocks = (n + 2 * kBlock - 1) / (2 * kBlock);  // two signatures per lane
   if (blocks > ws_slots) blocks = ws_slots;
-  if (mode == kStrict)
-    launch_verify_mode<kStrict>(blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_combB, d_ws, d_out_words, s);
-  else
-    launch_verify_mode<kCofactorless>(blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_combB, d_ws,
-                                      d_out_words, s);
-  return hipGetLastError();
+  return mode == kStrict
+             ? launch_verify_m<kStrict>(blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_combB, d_ws, d_out_words, s)
+             : launch_verify_m<kCofactorless>(blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_combB, d_ws,
+                                              d_out_words, s);
 }
 
 hipError_t launch_group_and(const uint64_t* d_first, const uint32_t* d_cnt, uint64_t G,
@@ -408,20 +333,10 @@ hipError_t launch_verify_keyset(int mode, const uint32_t* d_key_idx, const uint8
                                 const uint32_t* d_combB, uint64_t* d_out_words, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const uint64_t blocks = (n + 2 * kBlock - 1) / (2 * kBlock);  // two signatures per lane
-  const bool o3 = keyset_occ() == 3;
-#define NT_KS_LAUNCH(M, O)                                                                                   \
-  hipLaunchKernelGGL((k_ed25519_verify_keyset<M, O>), dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_key_idx, \
-                     (const uint32_t*)d_sig, d_msg, d_off, d_len, n, d_meta, d_enc, d_combA, nkeys, d_combB,  \
-                     (unsigned long long*)d_out_words)
-  if (mode == kStrict) {
-    if (o3) NT_KS_LAUNCH(kStrict, 3);
-    else NT_KS_LAUNCH(kStrict, 2);
-  } else {
-    if (o3) NT_KS_LAUNCH(kCofactorless, 3);
-    else NT_KS_LAUNCH(kCofactorless, 2);
-  }
-#undef NT_KS_LAUNCH
-  return hipGetLastError();
+  return mode == kStrict ? launch_keyset_m<kStrict>(blocks, d_key_idx, d_sig, d_msg, d_off, d_len, n, d_meta,
+                                                    d_enc, d_combA, nkeys, d_combB, d_out_words, s)
+                         : launch_keyset_m<kCofactorless>(blocks, d_key_idx, d_sig, d_msg, d_off, d_len, n,
+                                                          d_meta, d_enc, d_combA, nkeys, d_combB, d_out_words, s);
 }
 
 size_t wcomb_bytes_per_key() { return kWWordsPerKey * 4; }

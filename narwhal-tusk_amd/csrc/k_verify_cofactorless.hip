@@ -1,0 +1,8 @@
+// k_verify_cofactorless.hip -- verify kernels, cofactorless mode (one translation unit per mode).
+#include "k_verify.inc"
+
+namespace nt {
+template hipError_t launch_verify_m<kCofactorless>(uint64_t, const uint8_t*, const uint8_t*, const uint8_t*,
+                                        const uint64_t*, const uint64_t*, uint64_t, const uint32_t*, void*,
+                                        uint64_t*, hipStream_t);
+}  // namespace nt

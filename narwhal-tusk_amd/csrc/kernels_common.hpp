@@ -1,0 +1,101 @@
+// kernels_common.hpp -- definitions shared by the gfx950 kernel translation
+// units (k_misc.hip, k_verify_*.hip, k_keyset_*.hip): block size, workspace
+// layout, table accessors, and the occupancy-variant switch.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "ed25519_ops.hpp"
+#include "kernels.hpp"
+
+namespace nt {
+
+constexpr int kBlock = 256;
+constexpr int kAEntries = 18;         // j*(+-A) and j*(-R), |digit| in 0..8
+constexpr int kAQuads = 10;           // uint4 per cached entry (40 words)
+
+// --------------------------------------------------------------------------
+// Table accessors
+// --------------------------------------------------------------------------
+// Wide comb of one point, layout [pos][entry][32 words]; 8 x 16-byte loads.
+struct WideComb {
+  const uint32_t* base;
+  NT_D NT_INLINE void load(uint32_t pos, uint32_t idx, ge_niels& q) const {
+    const uint4* e = (const uint4*)(base + ((size_t)pos * kWEntries + idx) * kWStride);
+    uint32_t w[32];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint4 v = e[i];
+      w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      q.ypx.v[i] = w[i];
+      q.ymx.v[i] = w[10 + i];
+      q.xy2d.v[i] = w[20 + i];
+    }
+  }
+};
+
+constexpr size_t kWWordsPerKey = (size_t)kWPos * kWEntries * kWStride;
+
+// j*(-A) entries in the global workspace, layout [slot][entry][quad][lane] of
+// uint4: a lane's 16-byte accesses are adjacent to its neighbours'.
+struct WsATab {
+  uint4* ws;
+  uint32_t slot;
+  NT_D NT_INLINE uint4* at(uint32_t entry) const {
+    return ws + ((size_t)(slot * kAEntries + entry) * kAQuads) * kBlock + threadIdx.x;
+  }
+  NT_D NT_INLINE void store(uint32_t entry, const ge_cached& c) const {
+    uint32_t w[40];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      w[i] = c.YpX.v[i]; w[10 + i] = c.YmX.v[i]; w[20 + i] = c.Z2.v[i]; w[30 + i] = c.T2d.v[i];
+    }
+    uint4* base = at(entry);
+#pragma unroll
+    for (int q = 0; q < kAQuads; ++q)
+      base[(size_t)q * kBlock] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  }
+  NT_D NT_INLINE void load(uint32_t entry, ge_cached& c) const {
+    uint32_t w[40];
+    const uint4* base = at(entry);
+#pragma unroll
+    for (int q = 0; q < kAQuads; ++q) {
+      const uint4 v = base[(size_t)q * kBlock];
+      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      c.YpX.v[i] = w[i]; c.YmX.v[i] = w[10 + i]; c.Z2.v[i] = w[20 + i]; c.T2d.v[i] = w[30 + i];
+    }
+  }
+};
+
+// Per-mode launchers, explicitly instantiated in k_verify_<mode>.hip and
+// k_keyset_<mode>.hip (one translation unit per kernel family and mode, so
+// the build compiles them in parallel); dispatched by launch_verify /
+// launch_verify_keyset in k_misc.hip.
+template <int MODE>
+hipError_t launch_verify_m(uint64_t blocks, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
+                           const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_combB,
+                           void* d_ws, uint64_t* d_out_words, hipStream_t s);
+template <int MODE>
+hipError_t launch_keyset_m(uint64_t blocks, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
+                           const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
+                           const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
+                           const uint32_t* d_combB, uint64_t* d_out_words, hipStream_t s);
+int keyset_occupancy();
+
+// Occupancy variants (waves per SIMD the register allocator targets), chosen
+// at run time for A/B measurement: NT_VERIFY_OCC in {1, 2, 3} (default 2),
+// NT_KEYSET_OCC in {2, 3} (default 3).
+inline int env_occ(const char* name, int dflt, int lo, int hi) {
+  const char* e = std::getenv(name);
+  const int v = e ? std::atoi(e) : dflt;
+  return v < lo || v > hi ? dflt : v;
+}
+
+}  // namespace nt

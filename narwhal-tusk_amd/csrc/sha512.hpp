@@ -1,7 +1,9 @@
 // sha512.hpp -- FIPS 180-4 SHA-512 for one lane per message on gfx950.
 //
-// 64-bit rotates lower to v_alignbit_b32 pairs, 64-bit adds to v_lshl_add_u64 /
-// v_add_co+v_addc, Ch/Maj to v_bfi_b32; big-endian word loads are byte-swapped
+// 64-bit rotates lower to v_alignbit_b32 pairs, 64-bit adds to v_lshl_add_u64,
+// the three-way XORs of the Sigma/sigma functions and Maj to gfx950's
+// v_bitop3_b32 (any 3-input boolean function in one instruction: 0x96 = XOR3,
+// 0xE8 = MAJ), Ch to v_bitop3/v_bfi; big-endian word loads are byte-swapped
 // with v_perm_b32.  The 16-entry circular message schedule keeps the state in
 // 8 + 16 64-bit registers (48 VGPRs).
 //
@@ -67,20 +69,50 @@ NT_HD NT_INLINE uint64_t shr64(uint64_t x) {
   return x >> N;
 #endif
 }
-// Maj(a,b,c) = bfi(a^b, c, b): one xor + one v_bfi_b32 per half
-NT_HD NT_INLINE uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) {
-  const uint64_t m = a ^ b;
+// 3-input boolean functions per 32-bit half: one v_bitop3_b32 each
+// (truth-table immediate indexed by (x << 2) | (y << 1) | z)
+template <int TT>
+NT_HD NT_INLINE uint64_t bitop3_64(uint64_t x, uint64_t y, uint64_t z) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t lo, hi;
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(lo) : "v"((uint32_t)m), "v"((uint32_t)c), "v"((uint32_t)b));
-  asm("v_bfi_b32 %0, %1, %2, %3"
-      : "=v"(hi)
-      : "v"((uint32_t)(m >> 32)), "v"((uint32_t)(c >> 32)), "v"((uint32_t)(b >> 32)));
+  const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)x, (uint32_t)y, (uint32_t)z, TT);
+  const uint32_t hi =
+      __builtin_amdgcn_bitop3_b32((uint32_t)(x >> 32), (uint32_t)(y >> 32), (uint32_t)(z >> 32), TT);
   return ((uint64_t)hi << 32) | lo;
 #else
-  return (m & c) | (~m & b);
+  uint64_t r = 0;
+  for (int i = 0; i < 8; ++i)
+    if ((TT >> i) & 1) {
+      const uint64_t mx = (i & 4) ? x : ~x, my = (i & 2) ? y : ~y, mz = (i & 1) ? z : ~z;
+      r |= mx & my & mz;
+    }
+  return r;
 #endif
 }
+// 64-bit add as one v_lshl_add_u64 behind an asm boundary: values rebuilt from
+// 32-bit halves (bitop3 / alignbit results) otherwise get their additions split
+// into half-width pieces by the optimizer (+25% instructions per block).
+NT_HD NT_INLINE uint64_t add64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t r;
+  asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+#else
+  return a + b;
+#endif
+}
+// a + K with K an SGPR pair
+NT_HD NT_INLINE uint64_t add64_s(uint64_t a, uint64_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t r;
+  asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(a), "s"(k));
+  return r;
+#else
+  return a + k;
+#endif
+}
+NT_HD NT_INLINE uint64_t xor3_64(uint64_t x, uint64_t y, uint64_t z) { return bitop3_64<0x96>(x, y, z); }
+NT_HD NT_INLINE uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) { return bitop3_64<0xE8>(a, b, c); }
+NT_HD NT_INLINE uint64_t ch64(uint64_t e, uint64_t f, uint64_t g) { return bitop3_64<0xCA>(e, f, g); }
 
 NT_HD NT_INLINE uint32_t bswap32(uint32_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -128,15 +160,15 @@ NT_HD NT_INLINE void sha_round(uint64_t v[8], uint64_t W[16]) {
   if constexpr (R >= 16) {
     constexpr int i = R & 15;
     const uint64_t w15 = W[(i + 1) & 15], w2 = W[(i + 14) & 15];
-    const uint64_t s0 = rotr64<1>(w15) ^ rotr64<8>(w15) ^ shr64<7>(w15);
-    const uint64_t s1 = rotr64<19>(w2) ^ rotr64<61>(w2) ^ shr64<6>(w2);
-    W[i] += s0 + W[(i + 9) & 15] + s1;
+    const uint64_t s0 = xor3_64(rotr64<1>(w15), rotr64<8>(w15), shr64<7>(w15));
+    const uint64_t s1 = xor3_64(rotr64<19>(w2), rotr64<61>(w2), shr64<6>(w2));
+    W[i] = add64(add64(W[i], s0), add64(W[(i + 9) & 15], s1));
   }
-  const uint64_t t1 = h + (rotr64<14>(e) ^ rotr64<18>(e) ^ rotr64<41>(e)) + ((e & f) | (~e & g)) +
-                      sha_k<R>() + W[R & 15];
-  const uint64_t t2 = (rotr64<28>(a) ^ rotr64<34>(a) ^ rotr64<39>(a)) + maj64(a, b, c);
-  d += t1;
-  h = t1 + t2;
+  const uint64_t kw = add64_s(W[R & 15], sha_k<R>());
+  const uint64_t t1 = add64(add64(h, kw), add64(xor3_64(rotr64<14>(e), rotr64<18>(e), rotr64<41>(e)), ch64(e, f, g)));
+  const uint64_t t2 = add64(xor3_64(rotr64<28>(a), rotr64<34>(a), rotr64<39>(a)), maj64(a, b, c));
+  d = add64(d, t1);
+  h = add64(t1, t2);
 }
 
 template <int R>
@@ -145,6 +177,65 @@ NT_HD NT_INLINE void sha_rounds(uint64_t v[8], uint64_t W[16]) {
     sha_round<R>(v, W);
     sha_rounds<R + 1>(v, W);
   }
+}
+
+// ---- split form for the producer/consumer kernel (k_sha512_pipe) ----
+// Producer: the 80 words K[t] + W[t] of one block, handed out in pairs.
+template <int R, class Sink>
+NT_HD NT_INLINE void sha_kw_pairs(uint64_t W[16], Sink& sink) {
+  if constexpr (R < 80) {
+    constexpr int i = R & 15;
+    if constexpr (R >= 16) {
+      const uint64_t w15 = W[(i + 1) & 15], w2 = W[(i + 14) & 15];
+      const uint64_t s0 = xor3_64(rotr64<1>(w15), rotr64<8>(w15), shr64<7>(w15));
+      const uint64_t s1 = xor3_64(rotr64<19>(w2), rotr64<61>(w2), shr64<6>(w2));
+      W[i] = add64(add64(W[i], s0), add64(W[(i + 9) & 15], s1));
+    }
+    const uint64_t kw0 = add64_s(W[i], sha_k<R>());
+    constexpr int j = (R + 1) & 15;
+    if constexpr (R + 1 >= 16) {
+      const uint64_t w15 = W[(j + 1) & 15], w2 = W[(j + 14) & 15];
+      const uint64_t s0 = xor3_64(rotr64<1>(w15), rotr64<8>(w15), shr64<7>(w15));
+      const uint64_t s1 = xor3_64(rotr64<19>(w2), rotr64<61>(w2), shr64<6>(w2));
+      W[j] = add64(add64(W[j], s0), add64(W[(j + 9) & 15], s1));
+    }
+    const uint64_t kw1 = add64_s(W[j], sha_k<R + 1>());
+    sink.template put<R / 2>(kw0, kw1);
+    sha_kw_pairs<R + 2>(W, sink);
+  }
+}
+
+// Consumer: one round given kw = K[t] + W[t].
+template <int R>
+NT_HD NT_INLINE void sha_round_kw(uint64_t v[8], uint64_t kw) {
+  uint64_t& a = v[(8 - R % 8) % 8];
+  uint64_t& b = v[(9 - R % 8) % 8];
+  uint64_t& c = v[(10 - R % 8) % 8];
+  uint64_t& d = v[(11 - R % 8) % 8];
+  uint64_t& e = v[(12 - R % 8) % 8];
+  uint64_t& f = v[(13 - R % 8) % 8];
+  uint64_t& g = v[(14 - R % 8) % 8];
+  uint64_t& h = v[(15 - R % 8) % 8];
+  const uint64_t t1 = add64(add64(h, kw), add64(xor3_64(rotr64<14>(e), rotr64<18>(e), rotr64<41>(e)), ch64(e, f, g)));
+  const uint64_t t2 = add64(xor3_64(rotr64<28>(a), rotr64<34>(a), rotr64<39>(a)), maj64(a, b, c));
+  d = add64(d, t1);
+  h = add64(t1, t2);
+}
+template <int R, class Source>
+NT_HD NT_INLINE void sha_rounds_kw(uint64_t v[8], const Source& src) {
+  if constexpr (R < 80) {
+    uint64_t kw0, kw1;
+    src.template get<R / 2>(kw0, kw1);
+    sha_round_kw<R>(v, kw0);
+    sha_round_kw<R + 1>(v, kw1);
+    sha_rounds_kw<R + 2>(v, src);
+  }
+}
+
+// big-endian message words of a block
+NT_HD NT_INLINE void sha512_block_w(uint64_t W[16], const uint32_t blk[32]) {
+#pragma unroll
+  for (int t = 0; t < 16; ++t) W[t] = ((uint64_t)bswap32(blk[2 * t]) << 32) | bswap32(blk[2 * t + 1]);
 }
 
 // One compression. blk[i] = LE 32-bit words of the 128-byte block as stored in memory.
@@ -158,7 +249,7 @@ NT_HD NT_INLINE void sha512_compress_words(uint64_t st[8], const uint32_t blk[32
   for (int i = 0; i < 8; ++i) v[i] = st[i];
   sha_rounds<0>(v, W);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) st[i] += v[i];
+  for (int i = 0; i < 8; ++i) st[i] = add64(st[i], v[i]);
 }
 
 // Load NW little-endian words starting at byte address p (any alignment) from

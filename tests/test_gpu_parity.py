@@ -74,6 +74,25 @@ def test_sha512_random_lengths_and_alignment(be):
         assert out[i].tobytes() == hashlib.sha512(m).digest()[:32], (i, int(lens[i]), int(off[i]))
 
 
+def test_sha512_both_kernels(be):
+    """n <= 32768 runs the two-wave producer/consumer kernel, larger n the
+    one-lane-per-message kernel: both against hashlib, with long and ragged
+    messages in the same call (lanes with different block counts)."""
+    rng = np.random.default_rng(7)
+    for n in (3, 1000, 33000):
+        lens = rng.integers(0, 300, n).astype(np.uint64)
+        lens[: min(n, 5)] = [0, 111, 112, 128, 2000][: min(n, 5)]
+        if n == 1000:
+            lens[17] = 70_000  # one lane runs ~550 blocks while the others stop early
+        off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+        data = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+        out = be.sha512_trunc32(data, off, lens)
+        raw = data.tobytes()
+        for i in range(n):
+            m = raw[int(off[i]):int(off[i] + lens[i])]
+            assert out[i].tobytes() == hashlib.sha512(m).digest()[:32], (n, i, int(lens[i]))
+
+
 def test_sha512_empty_input(be):
     out = be.sha512_trunc32(np.zeros(0, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint64))
     assert out.shape == (0, 32)
