@@ -14,7 +14,8 @@
 //   "R"  reduced   : output of mul/sq/carry: even limbs < 2^26, odd < 2^25 (+2^18 on limb 1)
 //   mul(f, g)      : f limbs < 2^28.6 (odd limbs get x2), g limbs < 2^27.75 (get x19)
 //                    => each term < 2^60.4, 10 terms < 2^63.8 < 2^64
-//   sq(f)          : f limbs < 2^27 (4f x 19f terms, <= 6 per column => < 2^62.8)
+//   sq(f)          : f even limbs < 2^26.1, odd < 2^25.1 (13 pre-scaled limbs)
+//   sq_wide(f)     : f limbs < 2^27 (4f x 19f terms, <= 6 per column => < 2^62.8)
 //   sub(f,g)       : f + 2p - g, needs g "R" (or sub4: f + 4p - g, g < 2^27 even / 2^26 odd)
 // Every point formula in ge25519.hpp is annotated with the bound it relies on.
 #pragma once
@@ -157,8 +158,9 @@ NT_HD NT_INLINE void fe_mul(fe& out, const fe& f, const fe& g) {
   NT_MUL_FENCE();
 }
 
-// h = f^2 using the symmetric products (55 instead of 100 multiplies).
-NT_HD NT_INLINE void fe_sq(fe& out, const fe& f) {
+// h = f^2 for an UNREDUCED f (limbs < 2^27, e.g. X + Y in ge_dbl): symmetric
+// products, 55 multiplies, coefficients split as (1|2|4) f_i x (1|19) f_j.
+NT_HD NT_INLINE void fe_sq_wide(fe& out, const fe& f) {
   NT_COUNT_SQ();
   uint32_t f2[10], f4[10], f19[10];
 #pragma unroll
@@ -184,6 +186,35 @@ NT_HD NT_INLINE void fe_sq(fe& out, const fe& f) {
       h[k] += (uint64_t)a * b;
     }
   }
+  fe_carry_wide(out, h);
+  NT_MUL_FENCE();
+}
+
+// h = f^2 for f with reduced-size limbs (even < 2^26.1, odd < 2^25.1: every
+// fe_mul / fe_sq / fe_carry output, plus small additions such as d y^2 + 1).
+// The odd-odd doubling is folded into 38 = 2 * 19 on the wrapped factor, so
+// only 13 limbs are pre-scaled (2 f_0..7, 38 f_5, 19 f_6, 38 f_7, 19 f_8,
+// 38 f_9 < 2^30.4); terms < 2^57.5, <= 6 per column.
+NT_HD NT_INLINE void fe_sq(fe& out, const fe& f) {
+  NT_COUNT_SQ();
+  const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
+  const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
+  const uint32_t f0_2 = 2u * f0, f1_2 = 2u * f1, f2_2 = 2u * f2, f3_2 = 2u * f3;
+  const uint32_t f4_2 = 2u * f4, f5_2 = 2u * f5, f6_2 = 2u * f6, f7_2 = 2u * f7;
+  const uint32_t f5_38 = 38u * f5, f6_19 = 19u * f6, f7_38 = 38u * f7, f8_19 = 19u * f8, f9_38 = 38u * f9;
+#define NT_M(a, b) ((uint64_t)(a) * (b))
+  uint64_t h[10];
+  h[0] = NT_M(f0, f0) + NT_M(f1_2, f9_38) + NT_M(f2_2, f8_19) + NT_M(f3_2, f7_38) + NT_M(f4_2, f6_19) + NT_M(f5, f5_38);
+  h[1] = NT_M(f0_2, f1) + NT_M(f2, f9_38) + NT_M(f3_2, f8_19) + NT_M(f4, f7_38) + NT_M(f5_2, f6_19);
+  h[2] = NT_M(f0_2, f2) + NT_M(f1_2, f1) + NT_M(f3_2, f9_38) + NT_M(f4_2, f8_19) + NT_M(f5_2, f7_38) + NT_M(f6, f6_19);
+  h[3] = NT_M(f0_2, f3) + NT_M(f1_2, f2) + NT_M(f4, f9_38) + NT_M(f5_2, f8_19) + NT_M(f6, f7_38);
+  h[4] = NT_M(f0_2, f4) + NT_M(f1_2, f3_2) + NT_M(f2, f2) + NT_M(f5_2, f9_38) + NT_M(f6_2, f8_19) + NT_M(f7, f7_38);
+  h[5] = NT_M(f0_2, f5) + NT_M(f1_2, f4) + NT_M(f2_2, f3) + NT_M(f6, f9_38) + NT_M(f7_2, f8_19);
+  h[6] = NT_M(f0_2, f6) + NT_M(f1_2, f5_2) + NT_M(f2_2, f4) + NT_M(f3_2, f3) + NT_M(f7_2, f9_38) + NT_M(f8, f8_19);
+  h[7] = NT_M(f0_2, f7) + NT_M(f1_2, f6) + NT_M(f2_2, f5) + NT_M(f3_2, f4) + NT_M(f8, f9_38);
+  h[8] = NT_M(f0_2, f8) + NT_M(f1_2, f7_2) + NT_M(f2_2, f6) + NT_M(f3_2, f5_2) + NT_M(f4, f4) + NT_M(f9, f9_38);
+  h[9] = NT_M(f0_2, f9) + NT_M(f1_2, f8) + NT_M(f2_2, f7) + NT_M(f3_2, f6) + NT_M(f4_2, f5);
+#undef NT_M
   fe_carry_wide(out, h);
   NT_MUL_FENCE();
 }

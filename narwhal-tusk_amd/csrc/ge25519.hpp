@@ -65,8 +65,8 @@ NT_HD NT_INLINE void ge_dbl(ge_cp& r, const ge_p2& p) {
   fe_sq(YY, p.Y);
   fe_sq(ZZ2, p.Z);
   fe_add(ZZ2, ZZ2, ZZ2);      // < 2^27
-  fe_add(t, p.X, p.Y);        // < 2^27 (sq input bound)
-  fe_sq(S, t);
+  fe_add(t, p.X, p.Y);        // < 2^27 (sq_wide input bound)
+  fe_sq_wide(S, t);
   fe_add(r.Y, YY, XX);        // Y' = YY + XX           < 2^27
   fe_sub(r.Z, YY, XX);        // Z' = YY - XX (2p)      < 2^27.6
   fe_sub4(r.X, S, r.Y);       // X' = S - Y'  (4p)      < 2^28.6 -> carry

@@ -55,6 +55,12 @@ def fe_sq(f):
     return list(o)
 
 
+def fe_sq_wide(f):
+    o = (ctypes.c_uint32 * 10)()
+    load().nth_fe_sq_wide(arr(f), o)
+    return list(o)
+
+
 def fe_tobytes(f):
     o = ctypes.create_string_buffer(32)
     load().nth_fe_tobytes(arr(f), o)

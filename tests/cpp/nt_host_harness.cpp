@@ -126,6 +126,12 @@ void nth_fe_sq(const uint32_t* f, uint32_t* out) {
   fe_sq(c, a);
   std::memcpy(out, c.v, 40);
 }
+void nth_fe_sq_wide(const uint32_t* f, uint32_t* out) {
+  fe a, c;
+  std::memcpy(a.v, f, 40);
+  fe_sq_wide(c, a);
+  std::memcpy(out, c.v, 40);
+}
 void nth_fe_carry(const uint32_t* f, uint32_t* out) {
   fe a;
   std::memcpy(a.v, f, 40);

@@ -23,7 +23,9 @@ F_MAX = [0xFFFFFB4 + 0x8000000 if i == 0 else (0xFFFFFFC + 0x8000000 if i % 2 ==
          for i in range(10)]                                   # fe_sub4 of (2x reduced) -> f side only
 G_MAX = [0x7FFFFDA + 0x4000000 if i == 0 else (0x7FFFFFE + 0x4000000 if i % 2 == 0 else 0x3FFFFFE + 0x2000000 + (1 << 18))
          for i in range(10)]                                   # fe_sub of reduced -> either side
-S_MAX = [2 * M26 if i % 2 == 0 else 2 * M25 + (1 << 18) for i in range(10)]  # sum of two reduced -> sq input
+S_MAX = [2 * M26 if i % 2 == 0 else 2 * M25 + (1 << 18) for i in range(10)]  # sum of two reduced -> sq_wide input
+# fe_sq contract: even limbs < 2^26.1, odd < 2^25.1 (reduced outputs, d y^2 + 1)
+R_MAX = [int(2 ** 26.1) - 1 if i % 2 == 0 else int(2 ** 25.1) - 1 for i in range(10)]
 
 
 def _is_reduced(limbs):
@@ -51,11 +53,16 @@ def test_fe_mul_extreme_bounds():
 
 def test_fe_sq_extreme_bounds():
     rng = random.Random(2)
-    cases = [S_MAX] + [_rand_limbs(rng, S_MAX) for _ in range(3000)]
-    for f in cases:
-        out = H.fe_sq(f)
-        assert H.value(out) % H.P == H.value(f) ** 2 % H.P
-        assert _is_reduced(out)
+    for sq, mx in ((H.fe_sq, R_MAX), (H.fe_sq_wide, S_MAX)):
+        cases = [mx] + [_rand_limbs(rng, mx) for _ in range(3000)]
+        for k in range(10):  # single-limb maxima
+            f = [0] * 10
+            f[k] = mx[k]
+            cases.append(f)
+        for f in cases:
+            out = sq(f)
+            assert H.value(out) % H.P == H.value(f) ** 2 % H.P
+            assert _is_reduced(out)
 
 
 def test_fe_tobytes_canonical():

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Profiles committed under profiles/ for a round (run on the GPU box):
+#   1. rocprofv3 --kernel-trace --stats of the default bench command
+#   2. PMC passes (tools/pmc_collect.sh) for cfg2 verify + cfg4 SHA-512
+# Usage: bash tools/profile_round.sh <tag>
+set -euo pipefail
+TAG=${1:-r01}
+OUT=gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run -- python3 bench.py > "$OUT/bench_under_rocprof.log" 2>&1
+echo "stats done"
+PMC_BENCH_ARGS="--no-certs" bash tools/pmc_collect.sh "$OUT/pmc"
+echo "pmc done"
