@@ -41,6 +41,8 @@ sys.path.insert(0, os.path.join(ROOT, "narwhal-tusk_amd"))
 METRIC = "Ed25519 verifies/sec + SHA-512 GB/s at 1/2/4/8 MI355X vs dalek host-core base"
 MAD_PEAK_TS = 256 * 4 * 64 * 2.4e9 / 4 / 1e12  # v_mad_u64_u32: 4 cycles per wave64 per SIMD
 HBM_PEAK_GBS = 8000.0
+PMC_PROFILE = os.path.join("r01", "pmc_v5.json")  # tools/profile_round.sh + tools/pmc_summarize.py
+SODIUM = "/opt/conda/lib/libsodium.so.23"
 
 
 def parse():
@@ -171,16 +173,23 @@ def main():
     # algorithmic multiply-accumulates per verify (counted by tests/cpp/opcount)
     mads = mads_per_verify(L)
     achieved = mads * n / (kernel_ms * 1e-3) / 1e12
-    prof = load_profile(os.path.join("r01", "pmc_cfg2.json"))
+    prof = load_profile(PMC_PROFILE)
     pv = (prof or {}).get("kernels", {}).get("verify", {})
+    pvl = pv.get("per_launch", {})
     roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": round(MAD_PEAK_TS, 2),
                 "unit": "Tmad/s (v_mad_u64_u32 32x32->64 multiply-accumulates)",
                 "frac": round(achieved / MAD_PEAK_TS, 4),
                 "traffic": pv.get("hbm_bytes_per_launch"),
-                "traffic_note": "HBM bytes per launch from rocprofv3 FETCH_SIZE*2 + WRITE_SIZE (profiles/r01/pmc_cfg2.json, "
-                                "same kernel build); algorithmic input is 608 B/verify" if pv else None,
+                "traffic_note": ("HBM bytes per launch from rocprofv3 FETCH_SIZE*2 + WRITE_SIZE (profiles/%s, "
+                                 "same kernel build, separate --pmc passes); algorithmic input is 608 B/verify, the "
+                                 "rest is the per-lane [j]A/[j]R tables (~15 KB/verify) and spills" % PMC_PROFILE)
+                if pv else None,
                 "kernel": "k_ed25519_verify<strict>", "kernel_ms": round(kernel_ms, 3),
-                "mads_per_verify": mads}
+                "mads_per_verify": mads,
+                "valu_instr_per_verify": round(pvl["SQ_INSTS_VALU"] * 64 / pvl.get("n", n)) if "SQ_INSTS_VALU" in pvl else None,
+                "valu_issue_share": round(pv["valu_issue_share_4cyc"], 3) if "valu_issue_share_4cyc" in pv else None,
+                "issue_note": "the kernel is VALU-issue-bound (issue share from the PMC profile); non-mad VALU work "
+                              "(carries, pre-scaling, SHA-512, lattice reduction) is why mad frac < issue share"}
 
     line = {"metric": METRIC, "value": round(value, 1), "unit": "verifies/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
@@ -409,10 +418,50 @@ def cpu_baseline(args, pk_h, sig_h, msg_h, L, got):
     res = orc.verify_strict_many(pk_h[:sample], sig_h[:sample], msg_h[:sample * L], offs, lens, nthreads=th)
     dt = time.perf_counter() - t0
     agree = int((res.astype(bool) == got[:sample]).sum())
-    return {"value": round(sample / dt, 1), "unit": "verifies/s", "cores": th, "kind": "port",
-            "sample": "first %d of the same 1M cfg2 verifies (%.1f s wall on %d threads)" % (sample, dt, th),
-            "single_thread_us_per_verify": round(per * 1e6, 2),
-            "verdicts_agree_with_gpu": "%d/%d" % (agree, sample)}
+    out = {"value": round(sample / dt, 1), "unit": "verifies/s", "cores": th, "kind": "port",
+           "sample": "first %d of the same 1M cfg2 verifies (%.1f s wall on %d threads)" % (sample, dt, th),
+           "single_thread_us_per_verify": round(per * 1e6, 2),
+           "verdicts_agree_with_gpu": "%d/%d" % (agree, sample)}
+    ext = sodium_baseline(pk_h, sig_h, msg_h, L, got, th, args.cpu_seconds)
+    if ext:
+        out["external"] = ext
+    return out
+
+
+def sodium_baseline(pk_h, sig_h, msg_h, L, got, th, seconds):
+    """libsodium 1.0.18 crypto_sign_verify_detached (optimised C, ref10 arithmetic) on
+    the same inputs, th threads (ctypes releases the GIL): an external comparator
+    for the CPU baseline -- its verdicts coincide with verify_strict on this corpus
+    (SURVEY.md A.4), which is checked here too."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    if not os.path.exists(SODIUM):
+        return None
+    lib = ctypes.CDLL(SODIUM)
+    if lib.sodium_init() < 0:
+        return None
+    f = lib.crypto_sign_verify_detached
+    f.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_ulonglong, ctypes.c_char_p]
+    f.restype = ctypes.c_int
+    pkb, sgb, mb = pk_h.tobytes(), sig_h.tobytes(), msg_h.tobytes()
+
+    def run(lo, hi):
+        return [f(sgb[64 * i:64 * i + 64], mb[L * i:L * i + L], L, pkb[32 * i:32 * i + 32]) == 0 for i in range(lo, hi)]
+
+    t0 = time.perf_counter()
+    run(0, 256)
+    per = (time.perf_counter() - t0) / 256
+    sample = int(min(len(pk_h), max(th * 64, seconds / per)))
+    chunks = [(sample * j // th, sample * (j + 1) // th) for j in range(th)]
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(th) as ex:
+        res = [x for part in ex.map(lambda c: run(*c), chunks) for x in part]
+    dt = time.perf_counter() - t0
+    agree = int((np.array(res, bool) == got[:sample]).sum())
+    return {"name": "libsodium 1.0.18 crypto_sign_verify_detached", "value": round(sample / dt, 1),
+            "unit": "verifies/s", "cores": th, "kind": "external",
+            "sample": "first %d of the same cfg2 verifies (%.1f s wall)" % (sample, dt),
+            "single_thread_us_per_verify": round(per * 1e6, 2), "verdicts_agree_with_gpu": "%d/%d" % (agree, sample)}
 
 
 def mads_per_verify(msg_len):
