@@ -422,42 +422,33 @@ def cpu_baseline(args, pk_h, sig_h, msg_h, L, got):
            "sample": "first %d of the same 1M cfg2 verifies (%.1f s wall on %d threads)" % (sample, dt, th),
            "single_thread_us_per_verify": round(per * 1e6, 2),
            "verdicts_agree_with_gpu": "%d/%d" % (agree, sample)}
-    ext = sodium_baseline(pk_h, sig_h, msg_h, L, got, th, args.cpu_seconds)
+    ext = sodium_baseline(orc, pk_h, sig_h, msg_h, L, got, th, args.cpu_seconds)
     if ext:
         out["external"] = ext
     return out
 
 
-def sodium_baseline(pk_h, sig_h, msg_h, L, got, th, seconds):
+def sodium_baseline(orc, pk_h, sig_h, msg_h, L, got, th, seconds):
     """libsodium 1.0.18 crypto_sign_verify_detached (optimised C, ref10 arithmetic) on
-    the same inputs, th threads (ctypes releases the GIL): an external comparator
-    for the CPU baseline -- its verdicts coincide with verify_strict on this corpus
-    (SURVEY.md A.4), which is checked here too."""
-    import ctypes
-    from concurrent.futures import ThreadPoolExecutor
+    the same inputs and th threads (oracle/sodium_batch.c: a pthread loop, library
+    dlopen'ed): an external comparator for the CPU baseline -- its verdicts coincide
+    with verify_strict on this corpus, which is checked here too."""
     if not os.path.exists(SODIUM):
         return None
-    lib = ctypes.CDLL(SODIUM)
-    if lib.sodium_init() < 0:
+    k = 256
+    offs = np.arange(k, dtype=np.uint64) * L
+    lens = np.full(k, L, np.uint64)
+    t0 = time.perf_counter()
+    if orc.sodium_verify_many(SODIUM, pk_h[:k], sig_h[:k], msg_h[:k * L], offs, lens, 1) is None:
         return None
-    f = lib.crypto_sign_verify_detached
-    f.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_ulonglong, ctypes.c_char_p]
-    f.restype = ctypes.c_int
-    pkb, sgb, mb = pk_h.tobytes(), sig_h.tobytes(), msg_h.tobytes()
-
-    def run(lo, hi):
-        return [f(sgb[64 * i:64 * i + 64], mb[L * i:L * i + L], L, pkb[32 * i:32 * i + 32]) == 0 for i in range(lo, hi)]
-
-    t0 = time.perf_counter()
-    run(0, 256)
-    per = (time.perf_counter() - t0) / 256
+    per = (time.perf_counter() - t0) / k
     sample = int(min(len(pk_h), max(th * 64, seconds / per)))
-    chunks = [(sample * j // th, sample * (j + 1) // th) for j in range(th)]
+    offs = np.arange(sample, dtype=np.uint64) * L
+    lens = np.full(sample, L, np.uint64)
     t0 = time.perf_counter()
-    with ThreadPoolExecutor(th) as ex:
-        res = [x for part in ex.map(lambda c: run(*c), chunks) for x in part]
+    res = orc.sodium_verify_many(SODIUM, pk_h[:sample], sig_h[:sample], msg_h[:sample * L], offs, lens, th)
     dt = time.perf_counter() - t0
-    agree = int((np.array(res, bool) == got[:sample]).sum())
+    agree = int((res.astype(bool) == got[:sample]).sum())
     return {"name": "libsodium 1.0.18 crypto_sign_verify_detached", "value": round(sample / dt, 1),
             "unit": "verifies/s", "cores": th, "kind": "external",
             "sample": "first %d of the same cfg2 verifies (%.1f s wall)" % (sample, dt),

@@ -95,6 +95,11 @@ void ntor_basepoint_mul(const uint8_t s32[32], uint8_t out32[32]);
  * generator T8 of order 8. */
 void ntor_torsion_point(int i, uint8_t out32[32]);
 
+/* External CPU comparator (bench.py cpu_baseline): libsodium crypto_sign_verify_detached
+ * over n signatures on nthreads threads, library dlopen'ed from libpath; -1 if absent. */
+int ntor_sodium_verify_many(const char *libpath, const uint8_t *pk32, const uint8_t *sig64, const uint8_t *msg,
+                            const uint64_t *off, const uint64_t *len, uint64_t n, int nthreads, uint8_t *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -105,6 +105,22 @@ class Oracle:
                                                  ctypes.c_int(nthreads))
         return np.unpackbits(bm, bitorder="little")[:n]
 
+    def sodium_verify_many(self, libpath, pk, sig, msg, off, ln, nthreads=1):
+        """libsodium crypto_sign_verify_detached over n signatures (external CPU
+        comparator, bench.py); None when libsodium is absent."""
+        n = len(off)
+        out = np.zeros(max(n, 1), np.uint8)
+        pk = np.ascontiguousarray(pk, np.uint8)
+        sig = np.ascontiguousarray(sig, np.uint8)
+        msg = np.ascontiguousarray(msg, np.uint8) if len(msg) else np.zeros(1, np.uint8)
+        off = np.ascontiguousarray(off, np.uint64)
+        ln = np.ascontiguousarray(ln, np.uint64)
+        self.lib.ntor_sodium_verify_many.restype = ctypes.c_int
+        rc = self.lib.ntor_sodium_verify_many(ctypes.c_char_p(libpath.encode()), _ptr(pk), _ptr(sig), _ptr(msg),
+                                              _ptr(off, _u64p), _ptr(ln, _u64p), ctypes.c_uint64(n),
+                                              ctypes.c_int(nthreads), _ptr(out))
+        return None if rc != 0 else out[:n]
+
     def verify_batch_groups(self, pk, sig, first, cnt, msg32, nthreads=1):
         G = len(cnt)
         nsig = len(pk)

@@ -181,3 +181,15 @@ def test_torsion_points(oracle):
     assert mine == sorted(meta["torsion_encodings"])
     for e in meta["small_order_encodings"]:
         assert oracle.point_is_small_order(bytes.fromhex(e))
+
+
+def test_sodium_comparator_matches_corpus(oracle):
+    """The bench's external CPU comparator (oracle/sodium_batch.c over libsodium)
+    gives the corpus' strict verdicts."""
+    lib = "/opt/conda/lib/libsodium.so.23"
+    if not os.path.exists(lib):
+        pytest.skip("libsodium not present")
+    d = np.load(os.path.join(GOLD, "ed25519_corpus.npz"))
+    r = oracle.sodium_verify_many(lib, d["pk"], d["sig"], d["msg"], d["off"], d["len"], 4)
+    assert r is not None
+    assert np.array_equal(r.astype(bool), d["strict"].astype(bool))
