@@ -1,0 +1,94 @@
+// capi.cpp -- C entry points of libntnarwhal.so for the Python tests and bench.py
+// (ctypes): the wire codec (CPU only) and the batched primary::Core ingestion
+// path of SURVEY §8(f).1/(f).2 (GPU through libntcrypto).  Not part of the
+// crypto crate's boundary (include/ntcrypto.h is).
+#include <cstring>
+#include <exception>
+#include <memory>
+
+#include "narwhal.hpp"
+#include "wire.hpp"
+
+namespace {
+struct CoreHandle {
+  primary::Committee committee;
+  std::unique_ptr<crypto::KeySet> keyset;
+  primary::Core core;
+};
+}  // namespace
+
+extern "C" {
+
+// Decode one bincode PrimaryMessage and encode it again.  Returns the encoded
+// length (<= cap written to out), -1 on a decode error, -2 if cap is too small.
+// `used` receives the number of input bytes the decoder consumed.
+int64_t ntn_wire_reencode(const uint8_t* data, uint64_t len, uint8_t* out, uint64_t cap, uint64_t* used) {
+  primary::PrimaryMessage m;
+  size_t u = 0;
+  if (!primary::decode(data, (size_t)len, m, &u)) return -1;
+  if (used) *used = u;
+  const auto v = primary::encode(m);
+  if (v.size() > cap) return -2;
+  std::memcpy(out, v.data(), v.size());
+  return (int64_t)v.size();
+}
+
+// Header digest (messages.rs:70-84) of a decoded bincode PrimaryMessage::Header
+// or ::Certificate, computed on the host preimage (CPU check of the layout);
+// returns the preimage length or -1.
+int64_t ntn_wire_header_preimage(const uint8_t* data, uint64_t len, uint8_t* out, uint64_t cap) {
+  primary::PrimaryMessage m;
+  if (!primary::decode(data, (size_t)len, m)) return -1;
+  const primary::Header& h = m.kind == primary::MsgKind::Certificate ? m.certificate.header : m.header;
+  const auto v = h.digest_preimage();
+  if (v.size() > cap) return -2;
+  std::memcpy(out, v.data(), v.size());
+  return (int64_t)v.size();
+}
+
+// Committee of n authorities (keys32[n][32], stake[n], workers 0..nworkers[i]-1),
+// Core state (gc_round, current header as bincode of a PrimaryMessage::Header,
+// may be null), optional committee key cache.  Returns null on failure.
+void* ntn_core_new(const uint8_t* keys32, const uint32_t* stakes, const uint32_t* nworkers, uint32_t n,
+                   uint64_t gc_round, const uint8_t* cur_header, uint64_t cur_len, int use_keyset) {
+  try {
+    auto h = std::make_unique<CoreHandle>();
+    for (uint32_t i = 0; i < n; ++i) {
+      crypto::PublicKey pk;
+      std::memcpy(pk.bytes.data(), keys32 + 32 * (size_t)i, 32);
+      primary::Authority a;
+      a.stake = stakes[i];
+      for (uint32_t w = 0; w < nworkers[i]; ++w) a.workers.insert(w);
+      h->committee.authorities[pk] = a;
+    }
+    if (cur_header) {
+      primary::PrimaryMessage m;
+      if (!primary::decode(cur_header, (size_t)cur_len, m) || m.kind != primary::MsgKind::Header) return nullptr;
+      h->core.current_header = m.header;
+    }
+    if (use_keyset) h->keyset = primary::committee_keyset(h->committee);
+    h->core.committee = &h->committee;
+    h->core.gc_round = gc_round;
+    h->core.cache = h->keyset.get();
+    return h.release();
+  } catch (const std::exception&) {
+    return nullptr;
+  }
+}
+
+void ntn_core_free(void* p) { delete (CoreHandle*)p; }
+
+// Core::ingest over n packed wire messages: out_codes[i] = primary::DagError.
+// Returns 0, or -2 on a backend failure (never reported as a verdict).
+int ntn_core_ingest(void* p, const uint8_t* data, const uint64_t* off, const uint64_t* len, uint64_t n,
+                    int threads, int32_t* out_codes, double* decode_seconds) {
+  try {
+    const auto r = ((CoreHandle*)p)->core.ingest(data, off, len, (size_t)n, threads, decode_seconds);
+    for (uint64_t i = 0; i < n; ++i) out_codes[i] = (int32_t)r[i];
+    return 0;
+  } catch (const std::exception&) {
+    return -2;
+  }
+}
+
+}  // extern "C"

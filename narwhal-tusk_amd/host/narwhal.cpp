@@ -1,7 +1,11 @@
 // narwhal.cpp -- primary/worker caller mirrors over the crypto mirror.
 #include "narwhal.hpp"
 
+#include <chrono>
 #include <cstring>
+#include <thread>
+
+#include "wire.hpp"
 
 namespace primary {
 
@@ -14,6 +18,10 @@ const char* to_string(DagError e) {
     case DagError::UnknownAuthority: return "UnknownAuthority";
     case DagError::AuthorityReuse: return "AuthorityReuse";
     case DagError::CertificateRequiresQuorum: return "CertificateRequiresQuorum";
+    case DagError::TooOld: return "TooOld";
+    case DagError::UnexpectedVote: return "UnexpectedVote";
+    case DagError::SerializationError: return "SerializationError";
+    case DagError::UnexpectedMessage: return "UnexpectedMessage";
   }
   return "?";
 }
@@ -218,9 +226,162 @@ std::vector<DagError> verify_certificates(const Committee& committee, const std:
   return res;
 }
 
+namespace {
+bool is_genesis(const Certificate& c, const Committee& committee) {
+  // Certificate::genesis(committee).contains(c): default header (zero id,
+  // round 0) of a committee member, compared by (id, round, origin)
+  static const Digest zero{};
+  return c.header.id == zero && c.round() == 0 && committee.authorities.count(c.origin());
+}
+}  // namespace
+
+std::vector<DagError> Core::sanitize_batch(const std::vector<PrimaryMessage>& msgs) const {
+  const Committee& cm = *committee;
+  const size_t n = msgs.size();
+  std::vector<DagError> res(n, DagError::Ok);
+  // 1) round filters (core.rs:307-310, 317-329, 339-342); collect digest preimages
+  enum Need : uint8_t { kNone, kHeader, kVote, kCert };
+  std::vector<Need> need(n, kNone);
+  std::vector<std::vector<uint8_t>> pre;
+  std::vector<size_t> pre_at(n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    const auto& m = msgs[i];
+    switch (m.kind) {
+      case MsgKind::Header:
+        if (m.header.round < gc_round) { res[i] = DagError::TooOld; break; }
+        need[i] = kHeader;
+        pre_at[i] = pre.size();
+        pre.push_back(m.header.digest_preimage());
+        break;
+      case MsgKind::Vote: {
+        const Vote& v = m.vote;
+        if (v.round < current_header.round) { res[i] = DagError::TooOld; break; }
+        if (!(v.id == current_header.id && v.origin == current_header.author && v.round == current_header.round)) {
+          res[i] = DagError::UnexpectedVote;
+          break;
+        }
+        need[i] = kVote;
+        pre_at[i] = pre.size();
+        pre.push_back(v.digest_preimage());
+        break;
+      }
+      case MsgKind::Certificate: {
+        const Certificate& c = m.certificate;
+        if (c.round() < gc_round) { res[i] = DagError::TooOld; break; }
+        if (is_genesis(c, cm)) break;
+        need[i] = kCert;
+        pre_at[i] = pre.size();
+        pre.push_back(c.header.digest_preimage());
+        pre.push_back(c.digest_preimage());
+        break;
+      }
+      case MsgKind::CertificatesRequest: res[i] = DagError::UnexpectedMessage; break;
+    }
+  }
+  const auto dig = crypto::sha512_digest_batch(pre);  // launch 1
+  // 2) host prechecks in the reference order; collect the signature work
+  std::vector<Digest> sd;
+  std::vector<PublicKey> sk;
+  std::vector<Signature> ss;
+  std::vector<size_t> s_of(n, SIZE_MAX);
+  std::vector<Digest> gd;
+  std::vector<const std::vector<std::pair<PublicKey, Signature>>*> groups;
+  std::vector<size_t> g_of(n, SIZE_MAX);
+  for (size_t i = 0; i < n; ++i) {
+    const auto& m = msgs[i];
+    if (need[i] == kHeader || need[i] == kCert) {
+      const Header& h = need[i] == kHeader ? m.header : m.certificate.header;
+      const DagError e = header_precheck(h, dig[pre_at[i]], cm);
+      if (e != DagError::Ok) { res[i] = e; continue; }
+      s_of[i] = sd.size();
+      sd.push_back(h.id);
+      sk.push_back(h.author);
+      ss.push_back(h.signature);
+      if (need[i] == kCert) {
+        const DagError q = quorum_check(m.certificate, cm);
+        if (q != DagError::Ok) { res[i] = q; s_of[i] = SIZE_MAX; continue; }
+        g_of[i] = gd.size();
+        gd.push_back(dig[pre_at[i] + 1]);
+        groups.push_back(&m.certificate.votes);
+      }
+    } else if (need[i] == kVote) {
+      if (cm.stake(m.vote.author) == 0) { res[i] = DagError::UnknownAuthority; continue; }
+      s_of[i] = sd.size();
+      sd.push_back(dig[pre_at[i]]);
+      sk.push_back(m.vote.author);
+      ss.push_back(m.vote.signature);
+    }
+  }
+  // 3) launch 2 (every header/vote signature) and launch 3 (every certificate's votes).
+  // A certificate whose header signature fails reports InvalidSignature either way,
+  // so its vote group may be checked in the same pass.
+  const auto sv = cache ? cache->verify_many(sd, sk, ss) : crypto::verify_many(sd, sk, ss);
+  const auto gv = groups.empty() ? std::vector<bool>{}
+                  : cache ? cache->verify_batch_many(gd, groups) : crypto::verify_batch_many(gd, groups);
+  for (size_t i = 0; i < n; ++i) {
+    if (s_of[i] != SIZE_MAX && !sv[s_of[i]]) res[i] = DagError::InvalidSignature;
+    else if (g_of[i] != SIZE_MAX && !gv[g_of[i]]) res[i] = DagError::InvalidSignature;
+  }
+  return res;
+}
+
+std::vector<DagError> Core::ingest(const uint8_t* data, const uint64_t* off, const uint64_t* len, size_t n,
+                                   int threads, double* decode_seconds) const {
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<PrimaryMessage> msgs(n);
+  std::vector<uint8_t> ok(n, 0);
+  if (threads < 1) threads = 1;
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads; ++t)
+    pool.emplace_back([&, t] {
+      for (size_t i = n * t / threads; i < n * (t + 1) / threads; ++i)
+        ok[i] = decode(data + off[i], (size_t)len[i], msgs[i]);
+    });
+  for (auto& th : pool) th.join();
+  if (decode_seconds)
+    *decode_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  std::vector<PrimaryMessage> good;
+  std::vector<size_t> idx;
+  good.reserve(n);
+  for (size_t i = 0; i < n; ++i)
+    if (ok[i]) {
+      idx.push_back(i);
+      good.push_back(std::move(msgs[i]));
+    }
+  std::vector<DagError> res(n, DagError::SerializationError);
+  const auto r = sanitize_batch(good);
+  for (size_t k = 0; k < idx.size(); ++k) res[idx[k]] = r[k];
+  return res;
+}
+
 }  // namespace primary
 
 namespace worker {
+
+size_t DigestBatcher::submit(const Processor& p, std::vector<uint8_t> serialized_batch) {
+  procs_.push_back(p);
+  batches_.push_back(std::move(serialized_batch));
+  return batches_.size() - 1;
+}
+
+std::vector<std::vector<uint8_t>> DigestBatcher::flush(std::vector<crypto::Digest>* digests) {
+  const auto dig = batch_digests(batches_);  // one SHA-512 launch for both streams
+  std::vector<std::vector<uint8_t>> out;
+  out.reserve(dig.size());
+  for (size_t i = 0; i < dig.size(); ++i) {
+    // the Processor's output message (processor.rs:40-48) around the batched digest
+    std::vector<uint8_t> msg;
+    const uint32_t tag = procs_[i].own_digest ? 0 : 1;
+    for (int b = 0; b < 4; ++b) msg.push_back((uint8_t)(tag >> (8 * b)));
+    msg.insert(msg.end(), dig[i].bytes.begin(), dig[i].bytes.end());
+    for (int b = 0; b < 4; ++b) msg.push_back((uint8_t)(procs_[i].id >> (8 * b)));
+    out.push_back(std::move(msg));
+  }
+  if (digests) *digests = dig;
+  procs_.clear();
+  batches_.clear();
+  return out;
+}
 
 std::vector<uint8_t> serialize_batch(const Batch& batch) {
   std::vector<uint8_t> v;

@@ -8,9 +8,11 @@
 //                                           (primary/src/core.rs:338-346):
 //                                           one GPU launch for every header signature and
 //                                           one for every certificate's votes
-//   worker::serialize_batch / batch_digest / Processor
+//   primary::Core::sanitize_batch / ingest  core.rs:306-411 batched (SURVEY §8(f).1, (f).2;
+//                                           bincode codec in wire.hpp)
+//   worker::serialize_batch / batch_digest / Processor / DigestBatcher
 //                                           worker/src/batch_maker.rs:117-119,
-//                                           worker/src/processor.rs:35-55
+//                                           worker/src/processor.rs:35-55 (§8(f).3)
 #pragma once
 #include <cstdint>
 #include <map>
@@ -40,6 +42,10 @@ enum class DagError {
   UnknownAuthority,
   AuthorityReuse,
   CertificateRequiresQuorum,
+  TooOld,               // core.rs:307-310, 317-320, 339-342
+  UnexpectedVote,       // core.rs:323-329
+  SerializationError,   // primary.rs:230 (bincode decode failure)
+  UnexpectedMessage,    // core.rs:384 (CertificatesRequest is not a Core message)
 };
 const char* to_string(DagError e);
 
@@ -103,6 +109,29 @@ std::vector<DagError> verify_certificates(const Committee& committee, const std:
 // KeySet over the committee's authorities (BTreeMap order).
 std::unique_ptr<crypto::KeySet> committee_keyset(const Committee& committee);
 
+struct PrimaryMessage;  // wire.hpp
+
+// Caller-level batching of primary::Core (core.rs:306-411): the
+// Core's sanitize_header / sanitize_vote / sanitize_certificate over a whole
+// drained batch of messages, with the same verdict per message as calling them
+// one at a time, but every digest in ONE SHA-512 launch, every header and vote
+// signature in ONE verify_strict launch and every certificate's votes in ONE
+// verify_batch launch.  (The reference's only state these checks read is the
+// GC round and the header currently being voted on.)
+struct Core {
+  const Committee* committee = nullptr;
+  Round gc_round = 0;
+  Header current_header;
+  const crypto::KeySet* cache = nullptr;  // committee key cache (§8(f).4), optional
+
+  std::vector<DagError> sanitize_batch(const std::vector<PrimaryMessage>& msgs) const;
+  // wire ingestion (§8(f).2): bincode bytes of n PrimaryMessages (packed, off/len)
+  // -> decode on `threads` host threads (failure: SerializationError) -> sanitize_batch.
+  // decode_seconds (optional) receives the host decode time.
+  std::vector<DagError> ingest(const uint8_t* data, const uint64_t* off, const uint64_t* len, size_t n,
+                               int threads = 1, double* decode_seconds = nullptr) const;
+};
+
 }  // namespace primary
 
 namespace worker {
@@ -121,6 +150,23 @@ struct Processor {
   uint32_t id;
   bool own_digest;
   std::vector<uint8_t> process(const std::vector<uint8_t>& serialized_batch, crypto::Digest* digest_out = nullptr) const;
+};
+
+// Worker digest batching: the two Processor tasks of a worker
+// (worker.rs:182-188 own batches, :227-233 others' batches) feed one batcher;
+// every flush hashes all queued batches in ONE SHA-512 launch and returns each
+// Processor's output message in submission order.
+class DigestBatcher {
+ public:
+  // queue one serialized batch for Processor p; returns its ticket
+  size_t submit(const Processor& p, std::vector<uint8_t> serialized_batch);
+  // hash everything queued (one launch) -> (ticket order) Processor::process outputs
+  std::vector<std::vector<uint8_t>> flush(std::vector<crypto::Digest>* digests = nullptr);
+  size_t pending() const { return batches_.size(); }
+
+ private:
+  std::vector<Processor> procs_;
+  std::vector<std::vector<uint8_t>> batches_;
 };
 
 }  // namespace worker

@@ -1,0 +1,213 @@
+"""SURVEY §8(f).1 + (f).2: the bincode wire codec of PrimaryMessage and the
+batched primary::Core sanitizer of the C++ mirror, against an independent
+Python model (tests/_wire.py) and the CPU oracle.
+
+CPU: codec round trips, canonicalisation (BTreeMap / BTreeSet semantics),
+rejection of malformed bytes, the header digest preimage.
+GPU: Core::ingest over a drained batch of headers, votes, certificates, a
+CertificatesRequest and garbage, every DagError outcome, with and without the
+committee key cache, vs. the model's per-message verdicts.
+"""
+import os
+import random
+import struct
+import sys
+
+import numpy as np
+import pytest
+
+import _wire as W
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "narwhal-tusk_amd"))
+from ntcrypto import narwhal as N  # noqa: E402
+
+
+def _rb(rng, n):
+    return bytes(rng.getrandbits(8) for _ in range(n))
+
+
+def _random_objects(rng, count):
+    keys = [_rb(rng, 32) for _ in range(6)]
+    out = []
+    for i in range(count):
+        kind = i % 4
+        if kind == 0:
+            h = W.Header(rng.choice(keys), rng.getrandbits(64), {_rb(rng, 32): rng.getrandbits(32)
+                                                                 for _ in range(rng.randrange(0, 5))},
+                         {_rb(rng, 32) for _ in range(rng.randrange(0, 5))}, sig=_rb(rng, 64))
+            out.append(h)
+        elif kind == 1:
+            out.append(W.Vote(_rb(rng, 32), rng.getrandbits(64), rng.choice(keys), rng.choice(keys), _rb(rng, 64)))
+        elif kind == 2:
+            h = W.Header(rng.choice(keys), rng.getrandbits(20), {_rb(rng, 32): 0}, {_rb(rng, 32)}, sig=_rb(rng, 64))
+            out.append(W.Certificate(h, [(rng.choice(keys), _rb(rng, 64)) for _ in range(rng.randrange(0, 8))]))
+        else:
+            out.append(([_rb(rng, 32) for _ in range(rng.randrange(0, 4))], rng.choice(keys)))
+    return out
+
+
+def test_wire_roundtrip_random():
+    rng = random.Random(11)
+    for obj in _random_objects(rng, 200):
+        m = W.message(obj)
+        r = N.wire_reencode(m)
+        assert r is not None and r[0] == m and r[1] == len(m)
+
+
+def test_wire_trailing_bytes_allowed():
+    m = W.message(_random_objects(random.Random(3), 1)[0])
+    r = N.wire_reencode(m + b"\x00\x01junk")
+    assert r is not None and r[0] == m and r[1] == len(m)
+
+
+def test_wire_btree_semantics():
+    """payload entries and parents in any wire order / with repeats decode to the
+    BTreeMap / BTreeSet the reference builds (last value wins for a repeated key)."""
+    rng = random.Random(5)
+    author, d1, d2, p1, p2 = (_rb(rng, 32) for _ in range(5))
+    body = W._str(W.b64(author)) + struct.pack("<Q", 9)
+    body += struct.pack("<Q", 3) + d2 + struct.pack("<I", 1) + d1 + struct.pack("<I", 2) + d2 + struct.pack("<I", 3)
+    body += struct.pack("<Q", 3) + p2 + p1 + p2
+    idd, sig = _rb(rng, 32), _rb(rng, 64)
+    wire = struct.pack("<I", 0) + body + idd + sig
+    canon = W.Header(author, 9, {d1: 2, d2: 3}, {p1, p2}, id_=idd, sig=sig)
+    assert N.wire_reencode(wire)[0] == W.message(canon)
+    assert N.wire_header_preimage(wire) == canon.preimage()
+
+
+def test_wire_rejects_malformed():
+    rng = random.Random(7)
+    objs = _random_objects(rng, 8)
+    for obj in objs:
+        m = W.message(obj)
+        for cut in range(len(m)):  # every truncation
+            assert N.wire_reencode(m[:cut]) is None, (type(obj), cut)
+    key = _rb(rng, 32)
+    vote = W.Vote(_rb(rng, 32), 1, key, key, _rb(rng, 64))
+    good = W.message(vote)
+    assert N.wire_reencode(good) is not None
+    bad_tag = struct.pack("<I", 4) + good[4:]
+    assert N.wire_reencode(bad_tag) is None
+    b64 = W.b64(key)
+    pos = good.index(b64)
+
+    def with_key(s):
+        return good[:pos - 8] + struct.pack("<Q", len(s)) + s + good[pos + len(b64):]
+
+    assert N.wire_reencode(with_key(b64)) is not None
+    assert N.wire_reencode(with_key(b64[:-4] + b"!!!=")) is None          # invalid symbol
+    assert N.wire_reencode(with_key(W.b64(key[:31]))) is None             # decodes to < 32 bytes
+    assert N.wire_reencode(with_key(b64[:-1])) is None                    # bad length
+    tail = b64[-2:-1]                                                      # non-zero unused bits
+    alt = bytes([b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/"[
+        (b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/".index(tail) | 1)]])
+    assert N.wire_reencode(with_key(b64[:-2] + alt + b"=")) is None
+    assert N.wire_reencode(with_key(b"\xff" * 44)) is None                # not UTF-8
+    longer = W.b64(key + b"\x07\x08\x09")                                  # >= 32 bytes: first 32 kept
+    r = N.wire_reencode(with_key(longer))
+    assert r is not None and r[0] == good
+    huge = struct.pack("<I", 2) + W.Header(key, 1, {}, set()).encode() + struct.pack("<Q", 1 << 60)
+    assert N.wire_reencode(huge) is None
+
+
+# ------------------------------------------------------------------ GPU: batched Core
+def _scenario(orc, rng):
+    seeds = [bytes([i + 1]) * 32 for i in range(7)]
+    keys = [orc.pubkey(s) for s in seeds]
+    sk = dict(zip(keys, seeds))
+    stakes = [1, 1, 1, 1, 2, 1, 0]  # the last authority has no voting rights
+    nworkers = [2] * 7
+    com = W.Committee(keys, stakes, nworkers)
+    stranger_seed = b"\x55" * 32
+    stranger = orc.pubkey(stranger_seed)
+    sk[stranger] = stranger_seed
+
+    def sign(pk, d):
+        return orc.sign(sk[pk], pk, d)
+
+    def header(author, rnd, nworker=0, bad_sig=False, bad_id=False):
+        h = W.Header(author, rnd, {_rb(rng, 32): nworker, _rb(rng, 32): 0}, {_rb(rng, 32) for _ in range(3)})
+        if bad_id:
+            h.id = _rb(rng, 32)
+        h.sig = sign(author, h.id)
+        if bad_sig:
+            h.sig = h.sig[:40] + bytes([h.sig[40] ^ 1]) + h.sig[41:]
+        return h
+
+    gc_round, cur_round = 5, 8
+    cur = header(keys[0], cur_round)
+
+    def vote(author, rnd=cur_round, target=cur, bad_sig=False):
+        v = W.Vote(target.id, rnd, target.author, author)
+        v.sig = sign(author, v.digest())
+        if bad_sig:
+            v.sig = v.sig[:33] + bytes([v.sig[33] ^ 4]) + v.sig[34:]
+        return v
+
+    def cert(h, voters, bad_vote=None):
+        c = W.Certificate(h, [])
+        d = c.digest()
+        for pk in voters:
+            s = sign(pk, d)
+            if bad_vote is not None and pk == bad_vote:
+                s = bytes(32) + s[32:]
+            c.votes.append((pk, s))
+        return c
+
+    objs = [
+        header(keys[1], 9), header(keys[2], 4), header(keys[1], 9, bad_sig=True),
+        header(keys[1], 9, bad_id=True), header(stranger, 9), header(keys[6], 9), header(keys[3], 9, nworker=5),
+        vote(keys[2]), vote(keys[3], rnd=7), vote(keys[4], target=header(keys[1], cur_round)),
+        vote(stranger), vote(keys[6]), vote(keys[5], bad_sig=True), vote(keys[1], rnd=9),
+        cert(header(keys[2], 9), keys[:5]), cert(header(keys[2], 3), keys[:5]),
+        cert(W.Header(keys[3], 0, {}, set(), id_=bytes(32)), []),                 # genesis
+        cert(header(keys[2], 9, bad_sig=True), keys[:5]), cert(header(keys[2], 9), keys[:3]),
+        cert(header(keys[2], 9), keys[:4] + [keys[1]]), cert(header(keys[2], 9), keys[:4] + [stranger]),
+        cert(header(keys[2], 9), keys[:5], bad_vote=keys[3]), cert(header(keys[5], 10), keys[1:6]),
+        ([_rb(rng, 32)], keys[1]),
+    ]
+    wires = [W.message(o) for o in objs] + [b"\x02\x00\x00\x00garbage", b""]
+    strict = lambda d, pk, s: orc.verify_strict(pk, s, d)
+    batch = lambda d, votes: orc.verify_batch([v[0] for v in votes], [v[1] for v in votes], d)
+    expect = [W.model_sanitize(com, gc_round, cur, o, strict, batch) for o in objs]
+    expect += [W.SERIALIZATION_ERROR, W.SERIALIZATION_ERROR]
+    return keys, stakes, nworkers, gc_round, cur, wires, expect
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("use_keyset", [True, False])
+def test_core_ingest_matches_model(use_keyset):
+    from _oracle import load
+    orc = load()
+    rng = random.Random(2024)
+    keys, stakes, nworkers, gc_round, cur, wires, expect = _scenario(orc, rng)
+    # every outcome is exercised
+    assert set(expect) == set(range(11))
+    core = N.Core(np.frombuffer(b"".join(keys), np.uint8), stakes, nworkers, gc_round, W.message(cur), use_keyset)
+    try:
+        got, _ = core.ingest(*N.pack(wires), threads=3)
+        names = N.DAG_ERRORS
+        assert [names[c] for c in got] == [names[c] for c in expect]
+        # the same messages one at a time give the same verdicts
+        for w, e in zip(wires, expect):
+            g, _ = core.ingest(*N.pack([w]), threads=1)
+            assert names[g[0]] == names[e]
+    finally:
+        core.close()
+
+
+@pytest.mark.gpu
+def test_core_genesis_certificates():
+    """With gc_round 0 the genesis certificate of a committee member is accepted
+    without signatures (messages.rs:191); a non-member's is not genesis."""
+    from _oracle import load
+    orc = load()
+    keys = [orc.pubkey(bytes([i + 1]) * 32) for i in range(4)]
+    core = N.Core(np.frombuffer(b"".join(keys), np.uint8), [1] * 4, [1] * 4, 0, None, True)
+    try:
+        gen = W.Certificate(W.Header(keys[2], 0, {}, set(), id_=bytes(32)), [])
+        other = W.Certificate(W.Header(orc.pubkey(b"\x77" * 32), 0, {}, set(), id_=bytes(32)), [])
+        got, _ = core.ingest(*N.pack([W.message(gen), W.message(other)]))
+        assert [N.DAG_ERRORS[c] for c in got] == ["Ok", "InvalidHeaderId"]
+    finally:
+        core.close()
