@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--committee", type=int, default=100)
     ap.add_argument("--no-certs", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-ingest", action="store_true")
+    ap.add_argument("--ingest-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-seconds of baseline work")
     ap.add_argument("--cpu-threads", type=int, default=16)
     return ap.parse_args()
@@ -210,6 +212,10 @@ def main():
     # ---------------------------------------------------------------- config 3: certificates
     if not args.no_certs:
         line["certificates"] = bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_ranks)
+
+    # ---------------------------------------------------------------- §8(f).2: wire ingestion
+    if not args.no_ingest:
+        line["ingest"] = bench_ingest(args, be, world, rank, local, max_over_ranks, barrier)
 
     # ---------------------------------------------------------------- CPU baseline (rank 0, N=1)
     if world == 1 and not args.no_cpu:
@@ -397,6 +403,95 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
             "workload": "cfg3: %d certificates, committee n=%d, %d votes + 1 header signature each, "
                         "%d-byte header preimage" % (G_total, nk, quorum, hlen),
             "scaling": "strong (certificates sharded over ranks)", **out}
+
+
+def bench_ingest(args, be, world, rank, local, max_over_ranks, barrier):
+    """SURVEY §8(f).1 + (f).2: config 3's certificates as the primary receives
+    them -- bincode PrimaryMessage::Certificate bytes (primary/src/primary.rs:230)
+    -- through the C++ mirror's batched primary::Core::ingest: host decode
+    straight into SoA buffers (16 threads), the Core's checks in the reference
+    order, one SHA-512 + one verify_strict + one verify_batch launch against the
+    committee key cache.  PCIe-inclusive host entry points: this is the
+    wire-to-verdict rate, not the resident-data kernel rate of `certificates`."""
+    import hashlib
+    import struct
+    from ntcrypto import dist as nd
+    from ntcrypto import narwhal as N
+
+    os.environ["NT_DEVICE"] = str(local)
+    nk = args.committee
+    quorum = 2 * nk // 3 + 1
+    glo, ghi = nd.shard(args.certs, world, rank)
+    G = ghi - glo
+    n_pay, n_par = 32, quorum
+    seeds = np.stack([np.frombuffer(hashlib.sha512(b"nt-bench-key" + struct.pack("<Q", i)).digest()[:32], np.uint8)
+                      for i in range(nk)])
+    pks = be.sign_batch(seeds)
+    b64 = np.frombuffer(b"".join(__import__("base64").b64encode(p.tobytes()) for p in pks), np.uint8).reshape(nk, 44)
+    rng = np.random.default_rng(4242 + rank)
+    author = rng.integers(0, nk, G)
+    rnd = rng.integers(1, 1 << 40, G, dtype=np.uint64)
+
+    def sorted_digests(k):
+        d = rng.integers(0, 256, (G, k, 32), dtype=np.uint8)
+        key = d[:, :, :8].copy().view(">u8")[:, :, 0]     # BTreeMap/BTreeSet order (8-byte prefix)
+        return np.take_along_axis(d, np.argsort(key, axis=1)[:, :, None], axis=1)
+
+    pay = np.zeros((G, n_pay, 36), np.uint8)
+    pay[:, :, :32] = sorted_digests(n_pay)               # worker id 0
+    par = sorted_digests(n_par)
+    rbytes = rnd.view(np.uint8).reshape(G, 8)
+    pre = np.concatenate([pks[author], rbytes, pay.reshape(G, -1), par.reshape(G, -1)], axis=1)
+    plen = pre.shape[1]
+    ids = be.sha512_trunc32(pre.reshape(-1), np.arange(G, dtype=np.uint64) * plen, np.full(G, plen, np.uint64))
+    _, hsig = be.sign_batch(seeds[author], ids.reshape(-1), np.arange(G, dtype=np.uint64) * 32,
+                            np.full(G, 32, np.uint64))
+    cpre = np.concatenate([ids, rbytes, pks[author]], axis=1)
+    cdig = be.sha512_trunc32(cpre.reshape(-1), np.arange(G, dtype=np.uint64) * 72, np.full(G, 72, np.uint64))
+    voters = np.argsort(rng.random((G, nk)), axis=1)[:, :quorum]
+    V = G * quorum
+    _, vsig = be.sign_batch(seeds[voters.reshape(-1)], cdig.reshape(-1),
+                            np.repeat(np.arange(G, dtype=np.uint64) * 32, quorum), np.full(V, 32, np.uint64))
+    vsig = vsig.reshape(G, quorum, 64)
+    bad = np.sort(rng.choice(G, size=max(1, G // 100), replace=False))
+    vsig[bad, rng.integers(0, quorum, len(bad)), 40] ^= 1
+
+    def u64(x):
+        return np.full((G, 8), 0, np.uint8) + np.frombuffer(struct.pack("<Q", x), np.uint8)
+
+    votes = np.concatenate([np.broadcast_to(u64(44)[:, None, :], (G, quorum, 8)), b64[voters], vsig], axis=2)
+    wire = np.concatenate([np.broadcast_to(np.array([2, 0, 0, 0], np.uint8), (G, 4)), u64(44), b64[author], rbytes,
+                           u64(n_pay), pay.reshape(G, -1), u64(n_par), par.reshape(G, -1), ids, hsig, u64(quorum),
+                           votes.reshape(G, -1)], axis=1)
+    wlen = wire.shape[1]
+    data = np.ascontiguousarray(wire).reshape(-1)
+    off = np.arange(G, dtype=np.uint64) * wlen
+    ln = np.full(G, wlen, np.uint64)
+    expect = np.zeros(G, np.int32)
+    expect[bad] = 1                                        # InvalidSignature
+    core = N.Core(pks, np.ones(nk, np.uint32), np.ones(nk, np.uint32), 0, None, True)
+    try:
+        core.ingest(data, off, ln, args.ingest_threads)    # warm-up (key cache, allocations)
+        steps = 3
+        barrier()
+        t0 = time.perf_counter()
+        dec = 0.0
+        for _ in range(steps):
+            got, d = core.ingest(data, off, ln, args.ingest_threads)
+            dec += d
+        wall = max_over_ranks(time.perf_counter() - t0)
+        phases = {k: round(v * 1e3, 2) for k, v in N.Core.last_stats().items()}
+    finally:
+        core.close()
+    mism = int(max_over_ranks(int((got != expect).sum())))
+    return {"value": round(args.certs * steps / wall, 1), "unit": "certificates/s",
+            "workload": "cfg3 as wire bytes: %d bincode PrimaryMessage::Certificate messages of %d B (n=%d "
+                        "committee, %d votes), Core::ingest -> DagError per message" % (args.certs, wlen, nk, quorum),
+            "ms_per_step": round(wall * 1e3 / steps, 3), "host_decode_ms": round(dec * 1e3 / steps, 3),
+            "decode_threads": args.ingest_threads, "wire_bytes_per_step": int(G * wlen),
+            "phase_ms_last_step": phases,
+            "note": "host decode into SoA + reference-order checks + 1 SHA-512, 1 verify_strict, 1 verify_batch "
+                    "launch (key cache), PCIe-inclusive", "mismatches_vs_expected": mism}
 
 
 def cpu_baseline(args, pk_h, sig_h, msg_h, L, got):

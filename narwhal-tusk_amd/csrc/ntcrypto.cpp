@@ -394,6 +394,48 @@ int nt_ed25519_verify_strict(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* si
   });
 }
 
+// Stage certificate groups [glo, ghi) contiguously into pinned host buffers:
+// per signature its key (kw bytes: 32-byte encoding or 4-byte key index) and
+// signature, message offset 32 * (group - glo) and length 32; per group its
+// compacted first / cnt.  Copies are split over host threads by signature count
+// (a config-3 batch stages ~0.6 GB; one thread would take ~50 ms of it).
+static void stage_groups(uint64_t glo, uint64_t ghi, const uint64_t* first, const uint32_t* cnt, size_t kw,
+                         const uint8_t* keys, const uint8_t* sig64, uint8_t* hkey, uint8_t* hsig, uint64_t* hoff,
+                         uint64_t* hlen, uint64_t* hfirst, uint32_t* hcnt) {
+  uint64_t e = 0;
+  for (uint64_t g = glo; g < ghi; ++g) {
+    hfirst[g - glo] = e;
+    hcnt[g - glo] = cnt[g];
+    e += cnt[g];
+  }
+  const uint64_t m = e;
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const unsigned T = m < (1u << 16) ? 1u : hw;
+  auto work = [&](unsigned t) {
+    // groups whose first compacted signature falls in this thread's share
+    const uint64_t slo = m * t / T, shi = m * (t + 1) / T;
+    uint64_t g = glo + (std::lower_bound(hfirst, hfirst + (ghi - glo), slo) - hfirst);
+    for (; g < ghi && hfirst[g - glo] < shi; ++g) {
+      const uint64_t e0 = hfirst[g - glo], c = cnt[g];
+      if (!c) continue;
+      std::memcpy(hkey + kw * e0, keys + kw * first[g], kw * c);
+      std::memcpy(hsig + 64 * e0, sig64 + 64 * first[g], 64 * c);
+      for (uint64_t q = 0; q < c; ++q) {
+        hoff[e0 + q] = 32 * (g - glo);
+        hlen[e0 + q] = 32;
+      }
+    }
+  };
+  if (T == 1) {
+    work(0);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < T; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+}
+
 int nt_ed25519_verify_batch_groups(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* sig64,
                                    const uint64_t* first, const uint32_t* cnt,
                                    const uint8_t* msg32, uint64_t G, uint8_t* out_group_bitmap,
@@ -425,20 +467,7 @@ int nt_ed25519_verify_batch_groups(nt_ctx* ctx, const uint8_t* pk32, const uint8
     uint64_t* hlen = dv.h[B_LEN].as<uint64_t>();
     uint64_t* hfirst = dv.h[B_FIRST].as<uint64_t>();
     uint32_t* hcnt = dv.h[B_CNT].as<uint32_t>();
-    uint64_t e = 0;
-    for (uint64_t g = glo; g < ghi; ++g) {
-      hfirst[g - glo] = e;
-      hcnt[g - glo] = cnt[g];
-      if (cnt[g]) {
-        std::memcpy(hpk + 32 * e, pk32 + 32 * first[g], 32ull * cnt[g]);
-        std::memcpy(hsig + 64 * e, sig64 + 64 * first[g], 64ull * cnt[g]);
-      }
-      for (uint32_t t = 0; t < cnt[g]; ++t) {
-        hoff[e + t] = 32 * (g - glo);
-        hlen[e + t] = 32;
-      }
-      e += cnt[g];
-    }
+    stage_groups(glo, ghi, first, cnt, 32, pk32, sig64, hpk, hsig, hoff, hlen, hfirst, hcnt);
     NT_CHK(dv.d[B_PK].ensure(mm * 32));
     NT_CHK(dv.d[B_SIG].ensure(mm * 64));
     NT_CHK(dv.d[B_OFF].ensure(mm * 8));
@@ -630,20 +659,8 @@ int nt_ed25519_verify_batch_groups_keyset(nt_ctx* ctx, const nt_keyset* ks, cons
     uint64_t* hlen = dv.h[B_LEN].as<uint64_t>();
     uint64_t* hfirst = dv.h[B_FIRST].as<uint64_t>();
     uint32_t* hcnt = dv.h[B_CNT].as<uint32_t>();
-    uint64_t e = 0;
-    for (uint64_t g = glo; g < ghi; ++g) {
-      hfirst[g - glo] = e;
-      hcnt[g - glo] = cnt[g];
-      if (cnt[g]) {
-        std::memcpy(hki + e, key_idx + first[g], 4ull * cnt[g]);
-        std::memcpy(hsig + 64 * e, sig64 + 64 * first[g], 64ull * cnt[g]);
-      }
-      for (uint32_t t = 0; t < cnt[g]; ++t) {
-        hoff[e + t] = 32 * (g - glo);
-        hlen[e + t] = 32;
-      }
-      e += cnt[g];
-    }
+    stage_groups(glo, ghi, first, cnt, 4, (const uint8_t*)key_idx, sig64, (uint8_t*)hki, hsig, hoff, hlen, hfirst,
+                 hcnt);
     NT_CHK(dv.d[B_PK].ensure(mm * 4));
     NT_CHK(dv.d[B_SIG].ensure(mm * 64));
     NT_CHK(dv.d[B_OFF].ensure(mm * 8));

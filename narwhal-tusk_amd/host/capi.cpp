@@ -80,15 +80,30 @@ void ntn_core_free(void* p) { delete (CoreHandle*)p; }
 
 // Core::ingest over n packed wire messages: out_codes[i] = primary::DagError.
 // Returns 0, or -2 on a backend failure (never reported as a verdict).
+// general = 1: the object-model decoder + sanitize_batch (cross-check path).
 int ntn_core_ingest(void* p, const uint8_t* data, const uint64_t* off, const uint64_t* len, uint64_t n,
-                    int threads, int32_t* out_codes, double* decode_seconds) {
+                    int threads, int32_t* out_codes, double* decode_seconds, int general) {
   try {
-    const auto r = ((CoreHandle*)p)->core.ingest(data, off, len, (size_t)n, threads, decode_seconds);
+    const auto& core = ((CoreHandle*)p)->core;
+    const auto r = general ? core.ingest_general(data, off, len, (size_t)n, threads, decode_seconds)
+                           : core.ingest(data, off, len, (size_t)n, threads, decode_seconds);
     for (uint64_t i = 0; i < n; ++i) out_codes[i] = (int32_t)r[i];
     return 0;
   } catch (const std::exception&) {
     return -2;
   }
+}
+
+// phase times of the calling thread's last ingest: decode, prep, digest,
+// verify_strict, verify_batch, total (seconds)
+void ntn_last_ingest_stats(double out[6]) {
+  const auto& s = primary::last_ingest_stats();
+  out[0] = s.decode;
+  out[1] = s.prep;
+  out[2] = s.digest;
+  out[3] = s.strict;
+  out[4] = s.batch;
+  out[5] = s.total;
 }
 
 }  // extern "C"

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 
@@ -92,7 +93,12 @@ SecretKey SecretKey::decode_base64(const std::string& s) {
   return SecretKey(a);
 }
 
-Backend::Backend() { check(nt_init(&ctx_, 0), "nt_init"); }
+// every visible device, or only ordinal $NT_DEVICE (one process per GPU)
+Backend::Backend() {
+  const char* d = std::getenv("NT_DEVICE");
+  if (d && *d) check(nt_init_device(&ctx_, std::atoi(d)), "nt_init_device");
+  else check(nt_init(&ctx_, 0), "nt_init");
+}
 Backend::~Backend() {
   if (ctx_) nt_free(ctx_);
 }

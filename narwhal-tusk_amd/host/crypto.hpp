@@ -143,6 +143,7 @@ class KeySet {
   KeySet& operator=(const KeySet&) = delete;
   // index of `pk`, or UINT32_MAX if absent
   uint32_t index_of(const PublicKey& pk) const;
+  ::nt_keyset* handle() const { return ks_; }
   size_t size() const { return keys_.size(); }
   // verify_strict of (digest_i, key_i, sig_i) for keys in the set
   std::vector<bool> verify_many(const std::vector<Digest>& digests, const std::vector<PublicKey>& keys,

@@ -325,7 +325,7 @@ std::vector<DagError> Core::sanitize_batch(const std::vector<PrimaryMessage>& ms
   return res;
 }
 
-std::vector<DagError> Core::ingest(const uint8_t* data, const uint64_t* off, const uint64_t* len, size_t n,
+std::vector<DagError> Core::ingest_general(const uint8_t* data, const uint64_t* off, const uint64_t* len, size_t n,
                                    int threads, double* decode_seconds) const {
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<PrimaryMessage> msgs(n);

@@ -110,6 +110,13 @@ std::vector<DagError> verify_certificates(const Committee& committee, const std:
 std::unique_ptr<crypto::KeySet> committee_keyset(const Committee& committee);
 
 struct PrimaryMessage;  // wire.hpp
+struct IngestWorkspace;  // ingest.cpp
+
+// Phase times (seconds) of this thread's last Core::ingest (SoA path).
+struct IngestStats {
+  double decode = 0, prep = 0, digest = 0, strict = 0, batch = 0, total = 0;
+};
+IngestStats& last_ingest_stats();
 
 // Caller-level batching of primary::Core (core.rs:306-411): the
 // Core's sanitize_header / sanitize_vote / sanitize_certificate over a whole
@@ -123,13 +130,25 @@ struct Core {
   Round gc_round = 0;
   Header current_header;
   const crypto::KeySet* cache = nullptr;  // committee key cache (§8(f).4), optional
+  // staging reused across ingest calls (one ingest at a time per Core, like the
+  // reference's single Core task)
+  mutable std::shared_ptr<IngestWorkspace> ws;
 
   std::vector<DagError> sanitize_batch(const std::vector<PrimaryMessage>& msgs) const;
-  // wire ingestion (§8(f).2): bincode bytes of n PrimaryMessages (packed, off/len)
-  // -> decode on `threads` host threads (failure: SerializationError) -> sanitize_batch.
-  // decode_seconds (optional) receives the host decode time.
+  // wire ingestion (§8(f).2): bincode bytes of n PrimaryMessages (packed, off/len).
+  // ingest: flat decode straight into SoA launch buffers on `threads` host threads
+  // (ingest.cpp; failure: SerializationError), reference-order checks, 3 launches.
+  // ingest_general: decode into the object model (wire.cpp) + sanitize_batch --
+  // the same verdicts, kept as the cross-check.  decode_seconds (optional) gets
+  // the host decode time.
   std::vector<DagError> ingest(const uint8_t* data, const uint64_t* off, const uint64_t* len, size_t n,
-                               int threads = 1, double* decode_seconds = nullptr) const;
+                               int threads = 1, double* decode_seconds = nullptr) const {
+    return ingest_soa(data, off, len, n, threads, decode_seconds);
+  }
+  std::vector<DagError> ingest_soa(const uint8_t* data, const uint64_t* off, const uint64_t* len, size_t n,
+                                   int threads = 1, double* decode_seconds = nullptr) const;
+  std::vector<DagError> ingest_general(const uint8_t* data, const uint64_t* off, const uint64_t* len, size_t n,
+                                       int threads = 1, double* decode_seconds = nullptr) const;
 };
 
 }  // namespace primary

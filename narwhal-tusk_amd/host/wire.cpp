@@ -142,6 +142,10 @@ struct Reader {
 
 }  // namespace
 
+bool decode_public_key(const uint8_t* s, size_t len, PublicKey& out) {
+  return Reader::decode_key(std::string((const char*)s, len), out);
+}
+
 std::vector<uint8_t> encode_header(const Header& h) {
   Writer w;
   w.header(h);

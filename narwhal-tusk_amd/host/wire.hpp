@@ -37,6 +37,8 @@ struct PrimaryMessage {
 
 std::vector<uint8_t> encode(const PrimaryMessage& m);
 std::vector<uint8_t> encode_header(const Header& h);  // bincode of a bare Header
+// serde String + PublicKey::decode_base64 of the len bytes at s (false = error)
+bool decode_public_key(const uint8_t* s, size_t len, PublicKey& out);
 // false = bincode error (DagError::SerializationError); `used` = bytes consumed
 bool decode(const uint8_t* p, size_t n, PrimaryMessage& out, size_t* used = nullptr);
 

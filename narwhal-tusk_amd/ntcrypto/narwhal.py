@@ -42,8 +42,10 @@ def load():
         lib.ntn_core_free.argtypes = [ctypes.c_void_p]
         lib.ntn_core_free.restype = None
         lib.ntn_core_ingest.argtypes = [ctypes.c_void_p, _u8p, _u64p, _u64p, ctypes.c_uint64, ctypes.c_int,
-                                        ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)]
+                                        ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         lib.ntn_core_ingest.restype = ctypes.c_int
+        lib.ntn_last_ingest_stats.argtypes = [ctypes.POINTER(ctypes.c_double)]
+        lib.ntn_last_ingest_stats.restype = None
         _lib = lib
     return _lib
 
@@ -96,8 +98,9 @@ class Core:
         if not self._h:
             raise NtError("ntn_core_new failed (no gfx950 device, or a bad current header)")
 
-    def ingest(self, data, off, ln, threads=8):
-        """DagError codes for n packed wire messages; also returns the host decode seconds"""
+    def ingest(self, data, off, ln, threads=8, general=False):
+        """DagError codes for n packed wire messages; also returns the host decode
+        seconds.  general=True: the object-model decoder (cross-check path)."""
         n = len(off)
         codes = np.zeros(max(n, 1), np.int32)
         dec = ctypes.c_double(0)
@@ -106,10 +109,18 @@ class Core:
         ln = np.ascontiguousarray(ln, np.uint64)
         rc = load().ntn_core_ingest(self._h, data.ctypes.data_as(_u8p), off.ctypes.data_as(_u64p),
                                     ln.ctypes.data_as(_u64p), n, threads,
-                                    codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ctypes.byref(dec))
+                                    codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ctypes.byref(dec),
+                                    int(general))
         if rc != 0:
             raise NtError("ntn_core_ingest: backend failure")
         return codes[:n], dec.value
+
+    @staticmethod
+    def last_stats():
+        """phase seconds of the last SoA ingest on this thread"""
+        a = (ctypes.c_double * 6)()
+        load().ntn_last_ingest_stats(a)
+        return dict(zip(("decode", "prep", "digest", "verify_strict", "verify_batch", "total"), list(a)))
 
     def close(self):
         if self._h:

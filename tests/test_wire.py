@@ -167,10 +167,18 @@ def _scenario(orc, rng):
         ([_rb(rng, 32)], keys[1]),
     ]
     wires = [W.message(o) for o in objs] + [b"\x02\x00\x00\x00garbage", b""]
+    # a valid header whose payload entries arrive in descending order (non-canonical
+    # bytes: the decoder's BTreeMap sorts them, so the id still matches)
+    h = header(keys[3], 9)
+    body = h.encode()
+    a = 8 + 44 + 8 + 8
+    ents = [body[a + 36 * k:a + 36 * (k + 1)] for k in range(len(h.payload))]
+    wires.append(W.message(h)[:4] + body[:a] + b"".join(ents[::-1]) + body[a + 36 * len(ents):])
+    objs = objs + [None, None, h]
     strict = lambda d, pk, s: orc.verify_strict(pk, s, d)
     batch = lambda d, votes: orc.verify_batch([v[0] for v in votes], [v[1] for v in votes], d)
-    expect = [W.model_sanitize(com, gc_round, cur, o, strict, batch) for o in objs]
-    expect += [W.SERIALIZATION_ERROR, W.SERIALIZATION_ERROR]
+    expect = [W.model_sanitize(com, gc_round, cur, o, strict, batch) if o is not None else W.SERIALIZATION_ERROR
+              for o in objs]
     return keys, stakes, nworkers, gc_round, cur, wires, expect
 
 
@@ -185,9 +193,10 @@ def test_core_ingest_matches_model(use_keyset):
     assert set(expect) == set(range(11))
     core = N.Core(np.frombuffer(b"".join(keys), np.uint8), stakes, nworkers, gc_round, W.message(cur), use_keyset)
     try:
-        got, _ = core.ingest(*N.pack(wires), threads=3)
         names = N.DAG_ERRORS
-        assert [names[c] for c in got] == [names[c] for c in expect]
+        for general in (False, True):  # SoA fast path and the object-model path
+            got, _ = core.ingest(*N.pack(wires), threads=3, general=general)
+            assert [names[c] for c in got] == [names[c] for c in expect], general
         # the same messages one at a time give the same verdicts
         for w, e in zip(wires, expect):
             g, _ = core.ingest(*N.pack([w]), threads=1)
