@@ -42,6 +42,7 @@ METRIC = "Ed25519 verifies/sec + SHA-512 GB/s at 1/2/4/8 MI355X vs dalek host-co
 MAD_PEAK_TS = 256 * 4 * 64 * 2.4e9 / 4 / 1e12  # v_mad_u64_u32: 4 cycles per wave64 per SIMD
 HBM_PEAK_GBS = 8000.0
 PMC_PROFILE = os.path.join("r01", "pmc_v5.json")  # tools/profile_round.sh + tools/pmc_summarize.py
+PMC_N = 1_000_000  # signatures per launch in that profile (the default config-2 run)
 SODIUM = "/opt/conda/lib/libsodium.so.23"
 
 
@@ -50,7 +51,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1_000_000, help="signatures per GPU (config 2: 1M)")
+    ap.add_argument("--sigs", type=int, default=1_000_000, help="signatures per GPU (config 2: 1M)")
     ap.add_argument("--msg-len", type=int, default=512)
     ap.add_argument("--sha-msgs", type=int, default=16384, help="config 4 messages (total, sharded)")
     ap.add_argument("--sha-len", type=int, default=500_000)
@@ -101,7 +102,7 @@ def main():
         return nd.reduce_max(x)
 
     # ---------------------------------------------------------------- inputs (config 2)
-    n, L = args.n, args.msg_len
+    n, L = args.sigs, args.msg_len
     g = torch.Generator(device=dev)
     g.manual_seed(20241220 + rank)
     seeds = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device=dev, generator=g)
@@ -188,7 +189,7 @@ def main():
                 if pv else None,
                 "kernel": "k_ed25519_verify<strict>", "kernel_ms": round(kernel_ms, 3),
                 "mads_per_verify": mads,
-                "valu_instr_per_verify": round(pvl["SQ_INSTS_VALU"] * 64 / pvl.get("n", n)) if "SQ_INSTS_VALU" in pvl else None,
+                "valu_instr_per_verify": round(pvl["SQ_INSTS_VALU"] * 64 / PMC_N) if "SQ_INSTS_VALU" in pvl else None,
                 "valu_issue_share": round(pv["valu_issue_share_4cyc"], 3) if "valu_issue_share_4cyc" in pv else None,
                 "issue_note": "the kernel is VALU-issue-bound (issue share from the PMC profile); non-mad VALU work "
                               "(carries, pre-scaling, SHA-512, lattice reduction) is why mad frac < issue share"}
@@ -198,7 +199,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 limbs / u64 acc",
             "data": "synthetic (seeded random keys and 512-B messages, GPU-signed; 1% Appendix-B edge cases "
                     "from tests/golden/ed25519_corpus.npz)",
-            "config": {"workload": "cfg2: 1M verify_strict per GPU, 512-B messages, 1% edge mix",
+            "config": {"workload": "cfg2: %s verify_strict per GPU, %d-B messages, 1%% edge mix"
+                                   % ("1M" if n == 1_000_000 else str(n), L),
                        "n_per_gpu": n, "msg_len": L, "edge_cases": n_edge,
                        "parallelism": "shard-by-index, one process per GPU, no collective"},
             "roofline": roofline,
