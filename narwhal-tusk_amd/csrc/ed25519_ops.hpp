@@ -9,7 +9,7 @@
 //   verify_n<kStrict>         = PublicKey::verify_strict  (crypto/src/lib.rs:200-204)
 //   verify_n<kCofactorless>   = one entry of verify_batch under the deterministic
 //                               rule A.3                   (crypto/src/lib.rs:206-219)
-//   verify_cached_n<..>       = the same two predicates against a committee key cache
+//   verify_cached_batch<..>   = the same two predicates against a committee key cache
 //   sign_one                  = Keypair::generate + sign   (crypto/src/lib.rs:163-191)
 #pragma once
 #include "fe25519.hpp"
@@ -292,7 +292,7 @@ NT_HD NT_INLINE void hram_scalar(uint32_t k[8], const uint32_t Rw[8], const uint
 }
 
 // ---------------------------------------------------------------------------
-// Final comparison without decompressing R.  For R' = [s]B - [k]A with affine
+// Final comparison without decompressing R (key-cache path).  For R' = [s]B - [k]A with affine
 // (x', y'):
 //   dalek accepts  <=>  R decodes to a point equal to R'
 //                  <=>  y_R == y' (mod p)  and  (sign(R) == parity(x')  or  x' == 0)
@@ -300,7 +300,8 @@ NT_HD NT_INLINE void hram_scalar(uint32_t k[8], const uint32_t Rw[8], const uint
 // R' makes R decodable whenever y matches; x' = 0 covers the accepted
 // "negative zero" encodings).  In strict mode the small-order test of R is done
 // on R' (equal points have equal order; if they differ the verdict is reject
-// anyway).  With N = 2 the two Z^-1 come from one inversion (Montgomery's trick).
+// anyway).  verify_cached_batch gets the N Z^-1 of a lane from one inversion
+// (Montgomery's trick).
 // ---------------------------------------------------------------------------
 NT_HD NT_INLINE uint32_t enc_matches(const fe& x, const fe& y, const uint32_t Rw[8]) {
   fe yr;
@@ -317,31 +318,6 @@ NT_HD NT_INLINE uint32_t enc_matches(const fe& x, const fe& y, const uint32_t Rw
   }
   const uint32_t sign = Rw[7] >> 31;
   return same & (((xw[0] & 1u) == sign) | (xz == 0));
-}
-
-template <int MODE, int N>
-NT_HD NT_INLINE void finish_compare(uint32_t ok[N], const ge_p2 P[N], const uint32_t* const sig[N]) {
-  static_assert(N == 1 || N == 2, "one or two signatures per lane");
-  fe zi[N];
-  if (N == 1) {
-    fe_invert(zi[0], P[0].Z);
-  } else {
-    fe zz, inv;
-    fe_mul(zz, P[0].Z, P[N - 1].Z);
-    fe_invert(inv, zz);
-    fe_mul(zi[0], inv, P[N - 1].Z);
-    fe_mul(zi[N - 1], inv, P[0].Z);
-  }
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    fe x, y;
-    fe_mul(x, P[j].X, zi[j]);
-    fe_mul(y, P[j].Y, zi[j]);
-    uint32_t Rw[8];
-    ld8(Rw, sig[j]);
-    ok[j] &= enc_matches(x, y, Rw);
-    if (MODE == kStrict) ok[j] &= ge_is_small_order_p2(P[j]) ^ 1u;
-  }
 }
 
 // One verification (A, R, s encodings as words), half-size scalars:
@@ -404,41 +380,82 @@ NT_HD NT_INLINE void verify_n(uint32_t ok[N], const uint32_t* const A[N], const 
   }
 }
 
-// Key-cache variant: ca[j] is the wide comb of -A_j, meta[j] its kKey* bits.
+// Key-cache variant.  meta = the key's kKey* bits.
 enum : uint32_t { kKeyDecodes = 1u, kKeySmallOrder = 2u };
 
-template <int MODE, int N, class WCombA, class WCombB>
-NT_HD NT_INLINE void verify_cached_n(uint32_t ok[N], const uint32_t meta[N], const uint32_t* const A[N],
-                                     const uint32_t* const sig[N], const uint8_t* const msg[N],
-                                     const uint64_t len[N], const WCombA ca[N], const WCombB& cb) {
-  ge_p2 P[N];
+// One cached verification up to R' = [s]B - [k]A (extended), no decompression
+// of A and no doublings: 16 + 16 wide-comb additions.  Returns the s / key flags.
+template <int MODE, class WCombA, class WCombB>
+NT_HD NT_INLINE uint32_t cached_point(ge_p3& acc, uint32_t meta, const uint32_t Aw[8], const uint32_t Rw[8],
+                                      const uint32_t Sw[8], const uint8_t* msg, uint64_t len, const WCombA& ca,
+                                      const WCombB& cb) {
+  uint32_t okj = sc_is_canonical(Sw) & (meta & kKeyDecodes ? 1u : 0u);
+  if (MODE == kStrict) okj &= (meta & kKeySmallOrder) ? 0u : 1u;
+  uint32_t k[8];
+  hram_scalar(k, Rw, Aw, msg, len);
+  ge_p3_0(acc);
+  wcomb_acc(acc, k, ca);
+  wcomb_acc(acc, Sw, cb);
+  return okj;
+}
+
+// Compare of one projective R' with the encoding Rw given zi = Z^-1 (see
+// finish_compare); strict mode adds the small-order test on R'.
+template <int MODE>
+NT_HD NT_INLINE uint32_t compare_one(const ge_p2& P, const fe& zi, const uint32_t Rw[8]) {
+  fe x, y;
+  fe_mul(x, P.X, zi);
+  fe_mul(y, P.Y, zi);
+  uint32_t r = enc_matches(x, y, Rw);
+  if (MODE == kStrict) r &= ge_is_small_order_p2(P) ^ 1u;
+  return r;
+}
+
+// N cached verifications per lane with ONE inversion (Montgomery's trick).
+//   ld.get(j, meta, Aw, Rw, Sw, msg, len, ca)   inputs of signature j
+//   st.put(j, P, prefix) / st.get_point(j, P) /  per-lane stash of R'_j and the
+//   st.get_prefix(j, prefix)                     running product Z_0 .. Z_j
+// Returns bit j = verdict of signature j.  The stash keeps the registers of a
+// lane independent of N (the kernel's stash lives in global memory).
+template <int MODE, int N, class Loader, class WCombB, class Stash>
+NT_HD NT_INLINE uint32_t verify_cached_batch(const Loader& ld, const WCombB& cb, Stash& st) {
+  uint32_t okbits = 0;
+  fe acc;
 #pragma unroll 1
   for (int j = 0; j < N; ++j) {
-    const uint32_t* sj = pick<N>(sig, j);
-    const uint32_t mj = pick<N>(meta, j);
-    uint32_t Aw[8], Sw[8], k[8];
-    ld8(Aw, pick<N>(A, j));
-    ld8(Sw, sj + 8);
-    uint32_t okj = sc_is_canonical(Sw) & (mj & kKeyDecodes ? 1u : 0u);
-    if (MODE == kStrict) okj &= (mj & kKeySmallOrder) ? 0u : 1u;
-    {
-      uint32_t Rw[8];
-      ld8(Rw, sj);
-      hram_scalar(k, Rw, Aw, pick<N>(msg, j), pick<N>(len, j));
-    }
-    ge_p3 acc;
-    ge_p3_0(acc);
-    wcomb_acc(acc, k, pick<N>(ca, j));
-    wcomb_acc(acc, Sw, cb);
-#pragma unroll
-    for (int q = 0; q < N; ++q) {
-      if (q == j) {
-        ge_p3_to_p2(P[q], acc);
-        ok[q] = okj;
-      }
-    }
+    uint32_t meta, Aw[8], Rw[8], Sw[8];
+    const uint8_t* msg;
+    uint64_t len;
+    typename Loader::Comb ca;
+    ld.get(j, meta, Aw, Rw, Sw, msg, len, ca);
+    ge_p3 P;
+    okbits |= cached_point<MODE>(P, meta, Aw, Rw, Sw, msg, len, ca, cb) << j;
+    if (j == 0) acc = P.Z;
+    else fe_mul(acc, acc, P.Z);
+    ge_p2 P2;
+    ge_p3_to_p2(P2, P);
+    st.put(j, P2, acc);
   }
-  finish_compare<MODE, N>(ok, P, sig);
+  fe inv;
+  fe_invert(inv, acc);
+#pragma unroll 1
+  for (int j = N - 1; j >= 0; --j) {
+    ge_p2 P;
+    fe zi;
+    st.get_point(j, P);
+    if (j > 0) {
+      fe pre;
+      st.get_prefix(j - 1, pre);  // Z_0 .. Z_{j-1}
+      fe_mul(zi, inv, pre);
+      fe_mul(inv, inv, P.Z);
+    } else {
+      zi = inv;
+    }
+    uint32_t Rw[8];
+    ld.rbytes(j, Rw);
+    okbits &= ~((compare_one<MODE>(P, zi, Rw) ^ 1u) << j);
+  }
+  return okbits;
 }
 
 // Keygen + RFC 8032 signature.  sw = 32-byte seed words; wb = wide comb of B.

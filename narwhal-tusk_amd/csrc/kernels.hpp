@@ -23,7 +23,11 @@ hipError_t launch_wcomb_build(const uint32_t* d_enc, uint32_t nkeys, int negate,
 hipError_t launch_verify_keyset(int mode, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                                 const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                                 const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
-                                const uint32_t* d_combB, uint64_t* d_out_words, hipStream_t s);
+                                const uint32_t* d_combB, void* d_stash, uint64_t* d_out_words, hipStream_t s);
+// key-cache verification: blocks of a launch over n signatures and the per-lane
+// stash it needs (d_stash above)
+uint64_t keyset_blocks(uint64_t n);
+size_t keyset_stash_bytes(uint64_t n);
 size_t wcomb_bytes_per_key();
 size_t wcomb_bases_bytes_per_key();
 size_t wcomb_fill_tmp_bytes_per_key();

@@ -74,6 +74,45 @@ struct WsATab {
   }
 };
 
+// ---- key-cache verification: 4 signatures per lane, one inversion ----------
+constexpr int kKsPerLane = 4;
+constexpr int kKsQuads = 10;  // X, Y, Z, prefix: 40 words per (signature, lane)
+constexpr size_t kKsStashQuadsPerBlock = (size_t)kKsPerLane * kKsQuads * kBlock;
+
+// Per-lane stash in global memory, layout [block][j][quad][lane] of uint4
+// (lane-minor: a wave's 16-byte accesses are contiguous).
+struct KsStash {
+  uint4* base;  // this block's region
+  NT_D NT_INLINE uint4* at(int j, int q) const { return base + ((size_t)(j * kKsQuads + q) * kBlock + threadIdx.x); }
+  NT_D NT_INLINE void put(int j, const ge_p2& P, const fe& a) const {
+    uint32_t w[40];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) { w[i] = P.X.v[i]; w[10 + i] = P.Y.v[i]; w[20 + i] = P.Z.v[i]; w[30 + i] = a.v[i]; }
+#pragma unroll
+    for (int q = 0; q < kKsQuads; ++q) *at(j, q) = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  }
+  NT_D NT_INLINE void get_point(int j, ge_p2& P) const {
+    uint32_t w[32];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint4 v = *at(j, q);
+      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 10; ++i) { P.X.v[i] = w[i]; P.Y.v[i] = w[10 + i]; P.Z.v[i] = w[20 + i]; }
+  }
+  NT_D NT_INLINE void get_prefix(int j, fe& a) const {
+    uint32_t w[12];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const uint4 v = *at(j, 7 + q);
+      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 10; ++i) a.v[i] = w[2 + i];
+  }
+};
+
 // Per-mode launchers, explicitly instantiated in k_verify_<mode>.hip and
 // k_keyset_<mode>.hip (one translation unit per kernel family and mode, so
 // the build compiles them in parallel); dispatched by launch_verify /
@@ -86,7 +125,7 @@ template <int MODE>
 hipError_t launch_keyset_m(uint64_t blocks, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                            const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                            const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
-                           const uint32_t* d_combB, uint64_t* d_out_words, hipStream_t s);
+                           const uint32_t* d_combB, void* d_stash, uint64_t* d_out_words, hipStream_t s);
 int keyset_occupancy();
 
 // Occupancy variants (waves per SIMD the register allocator targets), chosen

@@ -70,7 +70,7 @@ struct HostBuf {
   T* as() const { return (T*)p; }
 };
 
-enum { B_DATA, B_OFF, B_LEN, B_PK, B_SIG, B_OUT, B_OUT2, B_FIRST, B_CNT, B_NBUF };
+enum { B_DATA, B_OFF, B_LEN, B_PK, B_SIG, B_OUT, B_OUT2, B_FIRST, B_CNT, B_STASH, B_NBUF };
 
 struct Device {
   int ordinal = -1;
@@ -615,10 +615,11 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
     NT_CHK(dv.h[B_OUT].ensure(words * 8));
     NT_TRY(hipMemcpyAsync(dv.d[B_PK].p, key_idx + lo, m * 4, hipMemcpyHostToDevice, dv.stream));
     NT_TRY(hipMemcpyAsync(dv.d[B_SIG].p, sig64 + 64 * lo, m * 64, hipMemcpyHostToDevice, dv.stream));
+    NT_CHK(dv.d[B_STASH].ensure(nt::keyset_stash_bytes(m)));
     NT_TRY(nt::launch_verify_keyset(mode, dv.d[B_PK].as<uint32_t>(), dv.d[B_SIG].as<uint8_t>(),
                                     dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>(),
                                     dv.d[B_LEN].as<uint64_t>(), m, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys,
-                                    dv.d_combB, dv.d[B_OUT].as<uint64_t>(), dv.stream));
+                                    dv.d_combB, dv.d[B_STASH].p, dv.d[B_OUT].as<uint64_t>(), dv.stream));
     NT_TRY(hipMemcpyAsync(dv.h[B_OUT].p, dv.d[B_OUT].p, words * 8, hipMemcpyDeviceToHost, dv.stream));
     NT_TRY(hipStreamSynchronize(dv.stream));
     words_to_bitmap(out_bitmap + lo / 8, dv.h[B_OUT].as<uint64_t>(), m);
@@ -681,10 +682,11 @@ int nt_ed25519_verify_batch_groups_keyset(nt_ctx* ctx, const nt_keyset* ks, cons
     NT_TRY(hipMemcpyAsync(dv.d[B_FIRST].p, hfirst, gm * 8, hipMemcpyHostToDevice, s));
     NT_TRY(hipMemcpyAsync(dv.d[B_CNT].p, hcnt, gm * 4, hipMemcpyHostToDevice, s));
     NT_TRY(hipMemsetAsync(dv.d[B_OUT].p, 0, sw * 8 + 8, s));
+    NT_CHK(dv.d[B_STASH].ensure(nt::keyset_stash_bytes(m)));
     NT_TRY(nt::launch_verify_keyset(NT_MODE_COFACTORLESS, dv.d[B_PK].as<uint32_t>(), dv.d[B_SIG].as<uint8_t>(),
                                     dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>(),
                                     dv.d[B_LEN].as<uint64_t>(), m, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys,
-                                    dv.d_combB, dv.d[B_OUT].as<uint64_t>(), s));
+                                    dv.d_combB, dv.d[B_STASH].p, dv.d[B_OUT].as<uint64_t>(), s));
     NT_TRY(nt::launch_group_and(dv.d[B_FIRST].as<uint64_t>(), dv.d[B_CNT].as<uint32_t>(), gm,
                                 dv.d[B_OUT].as<uint64_t>(), dv.d[B_OUT2].as<uint64_t>(), s));
     NT_TRY(hipMemcpyAsync(dv.h[B_OUT2].p, dv.d[B_OUT2].p, gw * 8, hipMemcpyDeviceToHost, s));
@@ -752,8 +754,16 @@ int nt_dev_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int dev, void
   NT_TRY(hipSetDevice(dv->ordinal));
   hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
   const auto& pd = ks->dev[dev];
+  // the device's stash: device-API key-cache launches on one device must be
+  // ordered on one stream (they share it)
+  void* stash;
+  {
+    std::lock_guard<std::mutex> lk(dv->mu);
+    NT_CHK(dv->d[B_STASH].ensure(nt::keyset_stash_bytes(n)));
+    stash = dv->d[B_STASH].p;
+  }
   NT_TRY(nt::launch_verify_keyset(mode, d_key_idx, d_sig64, d_msg, d_off, d_len, n, pd.d_meta, pd.d_enc, pd.d_comb,
-                                  ks->nkeys, dv->d_combB, d_out_words, s));
+                                  ks->nkeys, dv->d_combB, stash, d_out_words, s));
   return NT_OK;
 }
 

@@ -80,6 +80,20 @@ def verify_pair(mode, pk0, sig0, msg0, pk1, sig1, msg1, cached=False):
     return bool(out[0]), bool(out[1])
 
 
+def verify_cached4(mode, entries):
+    """Four (pk, sig, msg) through the key-cache kernel's path: 4 signatures per
+    lane, one inversion (verify_cached_batch<.., 4>)."""
+    assert len(entries) == 4
+    out = (ctypes.c_int * 4)()
+    msgs = [e[2] for e in entries]
+    mp = (ctypes.c_char_p * 4)(*msgs)
+    lens = (ctypes.c_uint64 * 4)(*[len(m) for m in msgs])
+    rc = load().nth_verify_cached_n(mode, 4, b"".join(e[0] for e in entries), b"".join(e[1] for e in entries),
+                                    mp, lens, out)
+    assert rc == 0
+    return tuple(bool(x) for x in out)
+
+
 def wcomb_chunk(enc, negate, pos, c):
     """Device wide-comb construction on the host: (meta, 65 x 32 words) for
     entries 64c .. 64c+64 of position pos (entry 64c only filled when c == 0)."""

@@ -204,28 +204,69 @@ void nth_verify_pair(int mode, const uint8_t* pk64, const uint8_t* sig128, const
   out2[0] = (int)ok[0];
   out2[1] = (int)ok[1];
 }
-// The key-cache path (combs of -A_j) for two signatures.
-void nth_verify_cached_pair(int mode, const uint8_t* pk64, const uint8_t* sig128, const uint8_t* m0, uint64_t l0,
-                            const uint8_t* m1, uint64_t l1, int* out2) {
-  alignas(16) uint32_t A[2][8], S[2][16];
-  std::memcpy(A, pk64, 64);
-  std::memcpy(S, sig128, 128);
-  static HostWComb ca[2];
+// The key-cache path (combs of -A_j) for nsig signatures (2 or 4: the kernel
+// runs 4 per lane) through verify_cached_batch with a host stash.
+struct HostStash {
+  ge_p2 P[4];
+  fe pre[4];
+  void put(int j, const ge_p2& p, const fe& a) { P[j] = p; pre[j] = a; }
+  void get_point(int j, ge_p2& p) const { p = P[j]; }
+  void get_prefix(int j, fe& a) const { a = pre[j]; }
+};
+struct HostCombRef {  // a comb by reference, with the WComb interface
+  const HostWComb* c;
+  void load(uint32_t pos, uint32_t idx, ge_niels& q) const { c->load(pos, idx, q); }
+};
+struct HostLoader {
+  using Comb = HostCombRef;
+  const uint32_t (*A)[8];
+  const uint32_t (*S)[16];
+  const uint8_t* const* M;
+  const uint64_t* L;
+  const uint32_t* meta;
+  HostWComb* ca;
+  void get(int j, uint32_t& m, uint32_t Aw[8], uint32_t Rw[8], uint32_t Sw[8], const uint8_t*& msg, uint64_t& len,
+           Comb& c) const {
+    m = meta[j];
+    for (int q = 0; q < 8; ++q) { Aw[q] = A[j][q]; Rw[q] = S[j][q]; Sw[q] = S[j][8 + q]; }
+    msg = M[j];
+    len = L[j];
+    c = HostCombRef{&ca[j]};
+  }
+  void rbytes(int j, uint32_t Rw[8]) const {
+    for (int q = 0; q < 8; ++q) Rw[q] = S[j][q];
+  }
+};
+int nth_verify_cached_n(int mode, int nsig, const uint8_t* pk, const uint8_t* sig, const uint8_t* const* msgs,
+                        const uint64_t* lens, int* out) {
+  if (nsig != 2 && nsig != 4) return -1;
+  alignas(16) uint32_t A[4][8], S[4][16];
+  std::memcpy(A, pk, 32 * nsig);
+  std::memcpy(S, sig, 64 * nsig);
+  static HostWComb ca[4];
   const unsigned long long cm = g_fe_mul, cs = g_fe_sq;  // key-cache build is not per signature
-  const uint32_t meta[2] = {key_comb(ca[0], A[0]), key_comb(ca[1], A[1])};
+  uint32_t meta[4];
+  for (int j = 0; j < nsig; ++j) {
+    meta[j] = key_comb(ca[j], A[j]);
+    ca[j].memo.clear();
+  }
   g_fe_mul = cm;
   g_fe_sq = cs;
-  ca[0].memo.clear();
-  ca[1].memo.clear();
-  const uint32_t* Ap[2] = {A[0], A[1]};
-  const uint32_t* Sp[2] = {S[0], S[1]};
-  const uint8_t* Mp[2] = {m0, m1};
-  const uint64_t Lp[2] = {l0, l1};
-  uint32_t ok[2];
-  if (mode == 0) verify_cached_n<kStrict, 2>(ok, meta, Ap, Sp, Mp, Lp, ca, bcomb());
-  else verify_cached_n<kCofactorless, 2>(ok, meta, Ap, Sp, Mp, Lp, ca, bcomb());
-  out2[0] = (int)ok[0];
-  out2[1] = (int)ok[1];
+  HostLoader ld{A, S, msgs, lens, meta, ca};
+  HostStash st;
+  uint32_t bits;
+  if (nsig == 2) bits = mode == 0 ? verify_cached_batch<kStrict, 2>(ld, bcomb(), st)
+                                  : verify_cached_batch<kCofactorless, 2>(ld, bcomb(), st);
+  else bits = mode == 0 ? verify_cached_batch<kStrict, 4>(ld, bcomb(), st)
+                        : verify_cached_batch<kCofactorless, 4>(ld, bcomb(), st);
+  for (int j = 0; j < nsig; ++j) out[j] = (bits >> j) & 1;
+  return 0;
+}
+void nth_verify_cached_pair(int mode, const uint8_t* pk64, const uint8_t* sig128, const uint8_t* m0, uint64_t l0,
+                            const uint8_t* m1, uint64_t l1, int* out2) {
+  const uint8_t* ms[2] = {m0, m1};
+  const uint64_t ls[2] = {l0, l1};
+  nth_verify_cached_n(mode, 2, pk64, sig128, ms, ls, out2);
 }
 void nth_sign(const uint8_t* seed, const uint8_t* msg, uint64_t len, uint8_t* pk, uint8_t* sig) {
   uint32_t sw[8], A[8], R[8], s[8];

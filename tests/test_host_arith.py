@@ -124,6 +124,23 @@ def test_corpus_pairs_through_device_code():
                 assert H.verify_pair(mode, *a, *b, cached=True) == want, (i, mode, "cached")
 
 
+def test_corpus_quads_through_keyset_path():
+    """The key-cache kernel's batch of 4 signatures per lane (one inversion for
+    all four, R'_j staged): every corpus entry in a quad with three neighbours."""
+    d = np.load(os.path.join(GOLD, "ed25519_corpus.npz"))
+    n = len(d["cat"])
+
+    def entry(i):
+        o, ln = int(d["off"][i]), int(d["len"][i])
+        return d["pk"][i].tobytes(), d["sig"][i].tobytes(), d["msg"][o:o + ln].tobytes()
+
+    for i in range(0, n, 4):
+        idx = [(i + k) % n for k in range(4)]
+        for mode, key in ((0, "strict"), (1, "batch_rule")):
+            want = tuple(bool(d[key][j]) for j in idx)
+            assert H.verify_cached4(mode, [entry(j) for j in idx]) == want, (i, mode)
+
+
 def _model():
     import importlib.util
     spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLD, "make_golden.py"))
