@@ -320,22 +320,14 @@ NT_HD NT_INLINE uint32_t enc_matches(const fe& x, const fe& y, const uint32_t Rw
   return same & (((xw[0] & 1u) == sign) | (xz == 0));
 }
 
-// One verification (A, R, s encodings as words), half-size scalars:
-//   ok  <=>  s < L, A and R decode, (strict) neither is small order, and
-//            [v s mod L]B - [u]A - [v]R == identity     (= [v]([s]B - [k]A - R))
-// with (u, v) = sc_halfsize(k), k = SHA-512(R || A || M) mod L.  at holds this
-// lane's tables, wb is the wide comb of B.
+// The check for a given lattice vector (u = (-1)^uneg |u|, v) of k with
+// max(bitlen |u|, bitlen v) <= bits; any valid vector gives the same verdict
+// (verify_one below uses sc_halfsize's; the tests also run the trivial (k, 1)).
 template <int MODE, class ATab, class WComb>
-NT_HD NT_INLINE uint32_t verify_one(const uint32_t Aw[8], const uint32_t Rw[8], const uint32_t Sw[8],
-                                    const uint8_t* msg, uint64_t len, ATab& at, const WComb& wb) {
+NT_HD NT_INLINE uint32_t verify_uv(const uint32_t Aw[8], const uint32_t Rw[8], const uint32_t Sw[8],
+                                   const uint32_t u[8], uint32_t uneg, const uint32_t v[8], int bits, ATab& at,
+                                   const WComb& wb) {
   uint32_t ok = sc_is_canonical(Sw);
-  uint32_t u[8], v[8], uneg;
-  int bits;
-  {
-    uint32_t k[8];
-    hram_scalar(k, Rw, Aw, msg, len);
-    bits = sc_halfsize(u, uneg, v, k);
-  }
   {
     ge_p3 A;
     ok &= ge_frombytes_w(A, Aw);
@@ -359,6 +351,24 @@ NT_HD NT_INLINE uint32_t verify_one(const uint32_t Aw[8], const uint32_t Rw[8], 
   ge_cp_to_p3(acc, t);
   wcomb_acc(acc, w, wb);
   return ok & fe_iszero(acc.X) & fe_eq(acc.Y, acc.Z);
+}
+
+// One verification (A, R, s encodings as words), half-size scalars:
+//   ok  <=>  s < L, A and R decode, (strict) neither is small order, and
+//            [v s mod L]B - [u]A - [v]R == identity     (= [v]([s]B - [k]A - R))
+// with (u, v) = sc_halfsize(k), k = SHA-512(R || A || M) mod L.  at holds this
+// lane's tables, wb is the wide comb of B.
+template <int MODE, class ATab, class WComb>
+NT_HD NT_INLINE uint32_t verify_one(const uint32_t Aw[8], const uint32_t Rw[8], const uint32_t Sw[8],
+                                    const uint8_t* msg, uint64_t len, ATab& at, const WComb& wb) {
+  uint32_t u[8], v[8], uneg;
+  int bits;
+  {
+    uint32_t k[8];
+    hram_scalar(k, Rw, Aw, msg, len);
+    bits = sc_halfsize(u, uneg, v, k);
+  }
+  return verify_uv<MODE>(Aw, Rw, Sw, u, uneg, v, bits, at, wb);
 }
 
 // N verifications per lane in turn.  A[j] = 8 pk words, sig[j] = 16 words

@@ -21,6 +21,8 @@ def load():
         subprocess.run(["make", "-s", "-C", CPP], check=True)
         _lib = ctypes.CDLL(LIB)
         _lib.nth_verify.restype = ctypes.c_int
+        _lib.nth_verify_trivial.restype = ctypes.c_int
+        _lib.nth_sc_halfsize.restype = ctypes.c_int
         _lib.nth_wcomb_chunk.restype = ctypes.c_uint32
         _lib.nth_count_mul.restype = ctypes.c_ulonglong
         _lib.nth_count_sq.restype = ctypes.c_ulonglong
@@ -80,6 +82,11 @@ def verify_pair(mode, pk0, sig0, msg0, pk1, sig1, msg1, cached=False):
     return bool(out[0]), bool(out[1])
 
 
+def verify_trivial(mode, pk, sig, msg):
+    """verify through the trivial lattice vector (k, 1): the 253-bit fallback ladder"""
+    return bool(load().nth_verify_trivial(mode, pk, sig, msg, ctypes.c_uint64(len(msg))))
+
+
 def verify_cached4(mode, entries):
     """Four (pk, sig, msg) through the key-cache kernel's path: 4 signatures per
     lane, one inversion (verify_cached_batch<.., 4>)."""
@@ -92,6 +99,16 @@ def verify_cached4(mode, entries):
                                     mp, lens, out)
     assert rc == 0
     return tuple(bool(x) for x in out)
+
+
+def sc_halfsize(k: int):
+    """(u, v, bits) from the device lattice reduction for k < 2^256 (u signed)"""
+    u = ctypes.create_string_buffer(32)
+    v = ctypes.create_string_buffer(32)
+    neg = ctypes.c_int(0)
+    bits = load().nth_sc_halfsize(k.to_bytes(32, "little"), u, v, ctypes.byref(neg))
+    uu = int.from_bytes(u.raw, "little")
+    return (-uu if neg.value else uu), int.from_bytes(v.raw, "little"), bits
 
 
 def wcomb_chunk(enc, negate, pos, c):

@@ -166,6 +166,16 @@ void nth_sc_muladd(const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t
   sc_muladd(r, wa, wb, wc);
   std::memcpy(out32, r, 32);
 }
+// sc_halfsize on a 32-byte scalar k: u, v (32 B each), sign of u; returns bits
+int nth_sc_halfsize(const uint8_t* k32, uint8_t* u32, uint8_t* v32, int* uneg) {
+  uint32_t k[8], u[8], v[8], un;
+  words(k, k32);
+  const int bits = sc_halfsize(u, un, v, k);
+  std::memcpy(u32, u, 32);
+  std::memcpy(v32, v, 32);
+  *uneg = (int)un;
+  return bits;
+}
 void nth_sha512(const uint8_t* msg, uint64_t len, uint8_t* out64) {
   uint64_t st[8];
   sha512_prefixed<0>(st, nullptr, msg, len);
@@ -186,6 +196,18 @@ int nth_verify(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   if (mode == 0) verify_n<kStrict, 1>(ok, Ap, Sp, Mp, Lp, at, bcomb());
   else verify_n<kCofactorless, 1>(ok, Ap, Sp, Mp, Lp, at, bcomb());
   return (int)ok[0];
+}
+// verify_uv with the trivial lattice vector (u, v) = (k, 1), 253-bit ladder:
+// the path sc_halfsize falls back to, checked against the same corpus.
+int nth_verify_trivial(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint64_t len) {
+  alignas(16) uint32_t A[8], S[16];
+  std::memcpy(A, pk, 32);
+  std::memcpy(S, sig, 64);
+  uint32_t k[8], v[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+  hram_scalar(k, S, A, msg, len);
+  HostATab at;
+  return (int)(mode == 0 ? verify_uv<kStrict>(A, S, S + 8, k, 0u, v, 253, at, bcomb())
+                         : verify_uv<kCofactorless>(A, S, S + 8, k, 0u, v, 253, at, bcomb()));
 }
 // Two signatures through the two-per-lane path the kernel runs (shared inversion).
 void nth_verify_pair(int mode, const uint8_t* pk64, const uint8_t* sig128, const uint8_t* m0, uint64_t l0,

@@ -124,6 +124,17 @@ def test_corpus_pairs_through_device_code():
                 assert H.verify_pair(mode, *a, *b, cached=True) == want, (i, mode, "cached")
 
 
+def test_corpus_through_fallback_ladder():
+    """The same verdicts through the trivial lattice vector (k, 1) -- the full
+    253-bit ladder sc_halfsize falls back to (step cap / oversized vectors)."""
+    d = np.load(os.path.join(GOLD, "ed25519_corpus.npz"))
+    for i in range(0, len(d["cat"]), 2):
+        o, n = int(d["off"][i]), int(d["len"][i])
+        pk, sig, m = d["pk"][i].tobytes(), d["sig"][i].tobytes(), d["msg"][o:o + n].tobytes()
+        assert H.verify_trivial(0, pk, sig, m) == bool(d["strict"][i]), i
+        assert H.verify_trivial(1, pk, sig, m) == bool(d["batch_rule"][i]), i
+
+
 def test_corpus_quads_through_keyset_path():
     """The key-cache kernel's batch of 4 signatures per lane (one inversion for
     all four, R'_j staged): every corpus entry in a quad with three neighbours."""
@@ -139,6 +150,29 @@ def test_corpus_quads_through_keyset_path():
         for mode, key in ((0, "strict"), (1, "batch_rule")):
             want = tuple(bool(d[key][j]) for j in idx)
             assert H.verify_cached4(mode, [entry(j) for j in idx]) == want, (i, mode)
+
+
+def test_sc_halfsize_properties():
+    """Half-size scalars (sc25519.hpp): for every k < L the result satisfies
+    u == v k (mod 8L), v odd, 0 < v < L, and bits >= bitlen(|u|), bitlen(v)
+    (the window count is never too small); typical sizes ~2^128.  Edge inputs
+    include k = 0, tiny k (loop not entered), k near L, powers of two and
+    values with huge partial quotients."""
+    L8 = 8 * H.L
+    rng = random.Random(9)
+    ks = [0, 1, 2, 7, 8, 9, H.L - 1, H.L - 2, H.L // 2, (H.L - 1) // 8, 1 << 127, (1 << 127) + 1, 1 << 128,
+          (1 << 200) + 12345, (1 << 252) - 1, H.L - (1 << 126), L8 // 3, L8 // 5]
+    ks += [(L8 * j) // (1 << 40) for j in range(1, 6)]          # huge first quotients
+    ks += [(L8 // q) + d for q in (3, 1 << 33, 1 << 70) for d in (-1, 0, 1)]
+    ks = [k % H.L for k in ks] + [rng.randrange(H.L) for _ in range(3000)]
+    big = 0
+    for k in ks:
+        u, v, bits = H.sc_halfsize(k)
+        assert (u - v * k) % L8 == 0, k
+        assert v % 2 == 1 and 0 < v < H.L, k
+        assert bits >= max(abs(u).bit_length(), v.bit_length()) and bits <= 253, k
+        big += bits > 136
+    assert big < 30  # random k: almost always ~128 bits
 
 
 def _model():
