@@ -101,7 +101,7 @@ int nt_ed25519_keypair_batch(nt_ctx *ctx, const uint8_t *seed32, uint64_t n, uin
 
 /* ---- committee key cache ------------------------------
  * A keyset holds, on every device of the context, per-key comb tables
- * (32 x 129 affine multiples of -A, 528 KiB per key) plus each key's raw
+ * (the 16-bit wide comb of -A: 16 x 32769 affine niels entries, 67 MB per key) plus each key's raw
  * encoding and decode / small-order flags, so verification against a static
  * committee (config/src/lib.rs:140-143) needs no decompression of A and no
  * doublings.  Keys are addressed by index (the caller's committee order);

@@ -1,5 +1,5 @@
 // ed25519_ops.hpp -- per-lane Ed25519 operations shared by the gfx950 kernels
-// (kernels.hip) and the host-compiled harness (tests/cpp/nt_host_harness.cpp,
+// (k_*.hip) and the host-compiled harness (tests/cpp/nt_host_harness.cpp,
 // tools/opcount.py).  Table storage is abstracted:
 //   ATab:  store(entry, ge_cached) / load(entry, ge_cached&)    j*(-A), j = 0..8, per lane
 //   WComb: load(pos, idx, ge_niels&)                            idx * 2^(16 pos) * P (wide comb)

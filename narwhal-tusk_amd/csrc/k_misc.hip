@@ -2,25 +2,27 @@
 // verification (which lives in k_verify_*.hip / k_keyset_*.hip), plus every
 // host launcher.  Kernel map of the library:
 //
-//   k_sha512_trunc32      one lane per message, Digest = SHA-512[..32]
+//   k_sha512_pipe         few long messages: producer wave (K+W into LDS) + consumer wave (rounds)
+//   k_sha512_trunc32      many messages: one lane per message, Digest = SHA-512[..32]
 //                         (worker/src/processor.rs:38; primary/src/messages.rs:70-84,145-153,226-234)
-//   k_ed25519_verify<M>   two signatures per lane; M = strict (crypto/src/lib.rs:200-204 ->
-//                         dalek verify_strict) or cofactorless (per-entry rule of
-//                         crypto/src/lib.rs:206-219 -> dalek verify_batch);
-//                         writes one verdict bit per signature (64-bit ballot words)
-//   k_ed25519_verify_keyset<M>  the same against a committee key cache (wide combs of -A)
+//   k_ed25519_verify<M>   two signatures per lane, half-size scalars; M = strict
+//                         (crypto/src/lib.rs:200-204 -> dalek verify_strict) or cofactorless
+//                         (per-entry rule of crypto/src/lib.rs:206-219 -> dalek verify_batch,
+//                         SURVEY.md A.3); one verdict bit per signature (64-bit ballot words)
+//   k_ed25519_verify_keyset<M>  the same against a committee key cache (wide combs of -A),
+//                         four signatures per lane sharing one inversion
 //   k_group_and           AND of per-signature bits over each certificate's vote range
 //   k_ed25519_sign        keygen + RFC 8032 signing (corpus generation / SignatureService
 //                         batch form; crypto/src/lib.rs:163-191) -- not constant time
 //   k_wcomb_bases/fill    wide-comb construction (B once per device, committee keys)
 //
 // SIMT design: every lane runs the same window schedule (fixed signed windows,
-// never per-lane sliding windows), so lanes of a wave never diverge inside the
-// scalar multiplications.  [s]B is 16 mixed additions from the 67 MB wide comb
-// of B (random 128-byte lines, the next one prefetched during the current
-// addition); [k](-A) uses 4-bit windows over a per-lane 9-entry cached table in
-// a global workspace laid out lane-minor so each lane's 16-byte accesses
-// coalesce across the workgroup.
+// a wave-uniform window count, never per-lane sliding windows), so lanes of a
+// wave never diverge inside the scalar multiplications.  [v s]B is 16 mixed
+// additions from the 67 MB wide comb of B (random 128-byte lines, the next one
+// prefetched during the current addition); [u](+-A) + [v](-R) use joint 4-bit
+// windows over per-lane 9-entry cached tables in a global workspace laid out
+// lane-minor so each lane's 16-byte accesses coalesce across the workgroup.
 #include "kernels_common.hpp"
 
 namespace nt {

@@ -1,4 +1,4 @@
-// kernels.hpp -- host-side launchers for kernels.hip (used by ntcrypto.cpp).
+// kernels.hpp -- host-side launchers of the k_*.hip kernels (used by ntcrypto.cpp).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>

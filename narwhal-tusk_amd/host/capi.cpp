@@ -94,6 +94,18 @@ int ntn_core_ingest(void* p, const uint8_t* data, const uint64_t* off, const uin
   }
 }
 
+// Core::ingest_pipelined: chunks of `chunk` messages, two in flight.
+int ntn_core_ingest_pipelined(void* p, const uint8_t* data, const uint64_t* off, const uint64_t* len, uint64_t n,
+                              int threads, uint64_t chunk, int32_t* out_codes) {
+  try {
+    const auto r = ((CoreHandle*)p)->core.ingest_pipelined(data, off, len, (size_t)n, threads, (size_t)chunk);
+    for (uint64_t i = 0; i < n; ++i) out_codes[i] = (int32_t)r[i];
+    return 0;
+  } catch (const std::exception&) {
+    return -2;
+  }
+}
+
 // phase times of the calling thread's last ingest: decode, prep, digest,
 // verify_strict, verify_batch, total (seconds)
 void ntn_last_ingest_stats(double out[6]) {

@@ -12,7 +12,9 @@
 // Messages whose payload / parents are not in canonical order (possible only
 // for hand-made bytes) take the general decoder + sanitize_batch; results are
 // identical either way (tests/test_wire.py compares both paths).
+#include <algorithm>
 #include <chrono>
+#include <exception>
 #include <cstring>
 #include <string_view>
 #include <thread>
@@ -500,6 +502,39 @@ std::vector<DagError> Core::ingest_soa(const uint8_t* data, const uint64_t* off,
     if (!((gbm[g / 8] >> (g % 8)) & 1)) res[all.gwho[g]] = DagError::InvalidSignature;
   st.total = since(t0);
   return res;  // a copy: the workspace keeps its buffers
+}
+
+std::vector<DagError> Core::ingest_pipelined(const uint8_t* data, const uint64_t* off, const uint64_t* len,
+                                             size_t n, int threads, size_t chunk) const {
+  if (chunk == 0 || chunk >= n) return ingest_soa(data, off, len, n, threads);
+  if (!ws) ws = std::make_shared<IngestWorkspace>();
+  if (!ws_alt) ws_alt = std::make_shared<IngestWorkspace>();
+  Core a = *this, b = *this;
+  b.ws = ws_alt;
+  std::vector<DagError> res(n);
+  const size_t K = (n + chunk - 1) / chunk;
+  auto run = [&](const Core& c, size_t k) {
+    const size_t lo = k * chunk, hi = std::min(n, lo + chunk);
+    const auto r = c.ingest_soa(data, off + lo, len + lo, hi - lo, threads);
+    std::copy(r.begin(), r.end(), res.begin() + lo);
+  };
+  std::exception_ptr err;
+  std::thread tb([&] {
+    try {
+      for (size_t k = 1; k < K; k += 2) run(b, k);
+    } catch (...) {
+      err = std::current_exception();
+    }
+  });
+  try {
+    for (size_t k = 0; k < K; k += 2) run(a, k);
+  } catch (...) {
+    tb.join();
+    throw;
+  }
+  tb.join();
+  if (err) std::rethrow_exception(err);
+  return res;
 }
 
 }  // namespace primary

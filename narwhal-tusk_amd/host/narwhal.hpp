@@ -132,7 +132,7 @@ struct Core {
   const crypto::KeySet* cache = nullptr;  // committee key cache (§8(f).4), optional
   // staging reused across ingest calls (one ingest at a time per Core, like the
   // reference's single Core task)
-  mutable std::shared_ptr<IngestWorkspace> ws;
+  mutable std::shared_ptr<IngestWorkspace> ws, ws_alt;
 
   std::vector<DagError> sanitize_batch(const std::vector<PrimaryMessage>& msgs) const;
   // wire ingestion (§8(f).2): bincode bytes of n PrimaryMessages (packed, off/len).
@@ -149,6 +149,11 @@ struct Core {
                                    int threads = 1, double* decode_seconds = nullptr) const;
   std::vector<DagError> ingest_general(const uint8_t* data, const uint64_t* off, const uint64_t* len, size_t n,
                                        int threads = 1, double* decode_seconds = nullptr) const;
+  // the batch in chunks of `chunk` messages, two chunks in flight on two
+  // workspaces: one chunk's host decode and checks overlap the other's GPU
+  // launches.  Same verdicts as ingest (messages are independent).
+  std::vector<DagError> ingest_pipelined(const uint8_t* data, const uint64_t* off, const uint64_t* len, size_t n,
+                                         int threads, size_t chunk) const;
 };
 
 }  // namespace primary

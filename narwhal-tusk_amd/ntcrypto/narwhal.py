@@ -44,6 +44,9 @@ def load():
         lib.ntn_core_ingest.argtypes = [ctypes.c_void_p, _u8p, _u64p, _u64p, ctypes.c_uint64, ctypes.c_int,
                                         ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         lib.ntn_core_ingest.restype = ctypes.c_int
+        lib.ntn_core_ingest_pipelined.argtypes = [ctypes.c_void_p, _u8p, _u64p, _u64p, ctypes.c_uint64, ctypes.c_int,
+                                                  ctypes.c_uint64, ctypes.POINTER(ctypes.c_int32)]
+        lib.ntn_core_ingest_pipelined.restype = ctypes.c_int
         lib.ntn_last_ingest_stats.argtypes = [ctypes.POINTER(ctypes.c_double)]
         lib.ntn_last_ingest_stats.restype = None
         _lib = lib
@@ -114,6 +117,20 @@ class Core:
         if rc != 0:
             raise NtError("ntn_core_ingest: backend failure")
         return codes[:n], dec.value
+
+    def ingest_pipelined(self, data, off, ln, threads=8, chunk=25000):
+        """Core::ingest_pipelined: chunks of `chunk` messages, two in flight"""
+        n = len(off)
+        codes = np.zeros(max(n, 1), np.int32)
+        data = np.ascontiguousarray(data, np.uint8)
+        off = np.ascontiguousarray(off, np.uint64)
+        ln = np.ascontiguousarray(ln, np.uint64)
+        rc = load().ntn_core_ingest_pipelined(self._h, data.ctypes.data_as(_u8p), off.ctypes.data_as(_u64p),
+                                              ln.ctypes.data_as(_u64p), n, threads, chunk,
+                                              codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        if rc != 0:
+            raise NtError("ntn_core_ingest_pipelined: backend failure")
+        return codes[:n]
 
     @staticmethod
     def last_stats():

@@ -197,6 +197,8 @@ def test_core_ingest_matches_model(use_keyset):
         for general in (False, True):  # SoA fast path and the object-model path
             got, _ = core.ingest(*N.pack(wires), threads=3, general=general)
             assert [names[c] for c in got] == [names[c] for c in expect], general
+        got = core.ingest_pipelined(*N.pack(wires), threads=2, chunk=5)  # two chunks in flight
+        assert [names[c] for c in got] == [names[c] for c in expect]
         # the same messages one at a time give the same verdicts
         for w, e in zip(wires, expect):
             g, _ = core.ingest(*N.pack([w]), threads=1)
