@@ -10,5 +10,5 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run -- python3 bench.py > "$OUT/bench_under_rocprof.log" 2>&1
 echo "stats done"
-PMC_BENCH_ARGS="--no-certs" bash tools/pmc_collect.sh "$OUT/pmc"
+PMC_BENCH_ARGS="--no-certs --no-ingest" bash tools/pmc_collect.sh "$OUT/pmc"
 echo "pmc done"
