@@ -329,24 +329,37 @@ hipError_t launch_wcomb_build(const uint32_t* d_enc, uint32_t nkeys, int negate,
   return hipSuccess;
 }
 
+// signatures per key-cache launch (a multiple of 64: verdict words stay aligned)
+constexpr uint64_t kKsMaxPerLaunch = 8ull << 20;
+
 hipError_t launch_verify_keyset(int mode, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                                 const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                                 const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
                                 const uint32_t* d_combB, void* d_stash, uint64_t* d_out_words, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  const uint64_t blocks = keyset_blocks(n);
-  return mode == kStrict ? launch_keyset_m<kStrict>(blocks, d_key_idx, d_sig, d_msg, d_off, d_len, n, d_meta,
-                                                    d_enc, d_combA, nkeys, d_combB, d_stash, d_out_words, s)
-                         : launch_keyset_m<kCofactorless>(blocks, d_key_idx, d_sig, d_msg, d_off, d_len, n,
-                                                          d_meta, d_enc, d_combA, nkeys, d_combB, d_stash,
-                                                          d_out_words, s);
+  // launches of at most kKsMaxPerLaunch signatures reuse one stash (stream-ordered)
+  for (uint64_t lo = 0; lo < n; lo += kKsMaxPerLaunch) {
+    const uint64_t m = n - lo < kKsMaxPerLaunch ? n - lo : kKsMaxPerLaunch;
+    const uint64_t blocks = keyset_blocks(m);
+    const hipError_t e =
+        mode == kStrict
+            ? launch_keyset_m<kStrict>(blocks, d_key_idx + lo, d_sig + 64 * lo, d_msg, d_off + lo, d_len + lo, m,
+                                       d_meta, d_enc, d_combA, nkeys, d_combB, d_stash, d_out_words + lo / 64, s)
+            : launch_keyset_m<kCofactorless>(blocks, d_key_idx + lo, d_sig + 64 * lo, d_msg, d_off + lo, d_len + lo,
+                                             m, d_meta, d_enc, d_combA, nkeys, d_combB, d_stash,
+                                             d_out_words + lo / 64, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 size_t wcomb_bytes_per_key() { return kWWordsPerKey * 4; }
 size_t wcomb_bases_bytes_per_key() { return (size_t)kWPos * 40 * 4; }
 size_t wcomb_fill_tmp_bytes_per_key() { return (size_t)kWPos * kWChunks * kWChunk * 10 * 4; }
 uint64_t keyset_blocks(uint64_t n) { return (n + kKsPerLane * kBlock - 1) / (kKsPerLane * kBlock); }
-size_t keyset_stash_bytes(uint64_t n) { return (size_t)keyset_blocks(n) * kKsStashQuadsPerBlock * 16; }
+// stash of one launch (<= kKsMaxPerLaunch signatures: 1.25 GiB at most)
+size_t keyset_stash_bytes(uint64_t n) {
+  return (size_t)keyset_blocks(n < kKsMaxPerLaunch ? n : kKsMaxPerLaunch) * kKsStashQuadsPerBlock * 16;
+}
 size_t ws_bytes_per_slot() { return (size_t)kAEntries * kAQuads * kBlock * 16; }
 
 }  // namespace nt

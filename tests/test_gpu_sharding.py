@@ -56,3 +56,27 @@ def test_sharded_batch_groups_and_keyset(pair):
     c = ks.verify_batch_groups(inv.astype(np.uint32).ravel(), g["sig"], g["first"], g["cnt"], g["msg32"])
     assert np.array_equal(c, g["expect"].astype(bool))
     ks.close()
+
+
+def test_keyset_launch_chunking(pair):
+    """More than 8 Mi signatures through the key cache: the launcher splits them
+    into launches of 8 Mi that reuse one per-lane stash; verdicts at the chunk
+    seam and at the ragged end must come out right."""
+    one, _ = pair
+    rng = np.random.default_rng(5)
+    seeds = rng.integers(0, 256, (4, 32), dtype=np.uint8)
+    msg = rng.integers(0, 256, 4 * 32, dtype=np.uint8)
+    pk, sig = one.sign_batch(seeds, msg, np.arange(4, dtype=np.uint64) * 32, np.full(4, 32, np.uint64))
+    ks = one.keyset(pk)
+    n = (8 << 20) + 1000
+    key = (np.arange(n) % 4).astype(np.uint32)
+    sigs = np.ascontiguousarray(sig[key])
+    off = (key.astype(np.uint64) * 32)
+    ln = np.full(n, 32, np.uint64)
+    bad = np.array([0, 5, (8 << 20) - 1, 8 << 20, (8 << 20) + 1, n - 1])
+    sigs[bad, 7] ^= 0x40
+    expect = np.ones(n, bool)
+    expect[bad] = False
+    got = ks.verify(0, key, sigs, msg, off, ln)
+    ks.close()
+    assert np.array_equal(got, expect)
