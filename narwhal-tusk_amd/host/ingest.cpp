@@ -195,9 +195,10 @@ struct Fast {
       r.vote_cnt = nv;
       for (uint64_t i = 0; ok && i < nv; ++i) {
         PublicKey raw;
-        a.vkey.push_back(key(raw));
+        const uint32_t k = key(raw);
         const uint8_t* sg = take(64);
         if (!ok) return;
+        a.vkey.push_back(k);
         a.vsig.push_back(sg);
       }
     } else {
@@ -257,8 +258,17 @@ std::vector<DagError> Core::ingest_soa(const uint8_t* data, const uint64_t* off,
   parallel_for(T, [&](int t) {
     for (size_t i = lo(t); i < hi(t); ++i) {
       Fast f{data + off[i], (size_t)len[i], 0, true, ki};
-      f.message(recs[i], arenas[t]);
-      if (!f.ok) recs[i].status = kRecBad;
+      Arena& a = arenas[t];
+      const size_t npre = a.pre.size(), nvote = a.vkey.size();
+      f.message(recs[i], a);
+      if (!f.ok) {
+        // drop whatever the failed message appended: vkey[k] and vsig[k] must
+        // stay the same vote for every later certificate of this thread
+        recs[i].status = kRecBad;
+        a.pre.resize(npre);
+        a.vkey.resize(nvote);
+        a.vsig.resize(nvote);
+      }
     }
   });
   if (decode_seconds) *decode_seconds = since(t0);

@@ -222,3 +222,66 @@ def test_core_genesis_certificates():
         assert [N.DAG_ERRORS[c] for c in got] == ["Ok", "InvalidHeaderId"]
     finally:
         core.close()
+
+
+def test_wire_decoder_fuzz():
+    """Untrusted network input: random mutations, truncations, splices and
+    garbage never crash the decoder, and whatever decodes re-encodes to a
+    canonical form that is a fixed point (decode(encode(m)) == m)."""
+    rng = random.Random(1234)
+    seeds = [W.message(o) for o in _random_objects(rng, 40)]
+    ok = 0
+    for it in range(6000):
+        m = bytearray(rng.choice(seeds))
+        op = it % 5
+        if op == 0:                       # flip random bytes
+            for _ in range(rng.randrange(1, 6)):
+                m[rng.randrange(len(m))] ^= 1 << rng.randrange(8)
+        elif op == 1:                     # overwrite a length / count field region with big values
+            p = rng.randrange(max(1, len(m) - 8))
+            m[p:p + 8] = struct.pack("<Q", rng.choice([0, 1, 44, 45, 1 << 32, (1 << 64) - 1, rng.getrandbits(64)]))
+        elif op == 2:                     # truncate
+            m = m[:rng.randrange(len(m))]
+        elif op == 3:                     # splice two messages
+            o = rng.choice(seeds)
+            m = m[:rng.randrange(len(m))] + o[rng.randrange(len(o)):]
+        else:                             # garbage with a valid tag
+            m = bytearray(struct.pack("<I", rng.randrange(5)) + bytes(rng.getrandbits(8) for _ in range(rng.randrange(200))))
+        r = N.wire_reencode(bytes(m))
+        if r is None:
+            continue
+        ok += 1
+        canon = r[0]
+        r2 = N.wire_reencode(canon)
+        assert r2 is not None and r2[0] == canon and r2[1] == len(canon)
+    assert ok > 100  # the mutations still leave many decodable messages
+
+
+@pytest.mark.gpu
+def test_core_soa_vs_general_fuzz():
+    """The SoA fast path (flat decode, key lookup by base64 text) and the
+    object-model path give identical DagErrors on mutated wire messages
+    (flipped bytes in keys, counts, digests and signatures; truncations)."""
+    from _oracle import load
+    orc = load()
+    rng = random.Random(77)
+    keys, stakes, nworkers, gc_round, cur, wires, _ = _scenario(orc, random.Random(2024))
+    core = N.Core(np.frombuffer(b"".join(keys), np.uint8), stakes, nworkers, gc_round, W.message(cur), True)
+    try:
+        batch = []
+        for it in range(3000):
+            m = bytearray(rng.choice(wires[:24]))
+            if not m:
+                continue
+            if it % 3 == 0:
+                m[rng.randrange(len(m))] ^= 1 << rng.randrange(8)
+            elif it % 3 == 1:
+                m = m[:rng.randrange(1, len(m) + 1)]
+            batch.append(bytes(m))
+        a, _ = core.ingest(*N.pack(batch), threads=4)
+        b, _ = core.ingest(*N.pack(batch), threads=4, general=True)
+        assert np.array_equal(a, b), [(i, N.DAG_ERRORS[x], N.DAG_ERRORS[y]) for i, (x, y) in enumerate(zip(a, b))
+                                      if x != y][:10]
+        assert len(set(a.tolist())) >= 6
+    finally:
+        core.close()
