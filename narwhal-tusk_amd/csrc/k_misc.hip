@@ -12,6 +12,7 @@
 //   k_ed25519_verify_keyset<M>  the same against a committee key cache (wide combs of -A),
 //                         four signatures per lane sharing one inversion
 //   k_group_and           AND of per-signature bits over each certificate's vote range
+//   k_group_msgs          per-signature message offset/length of certificate groups
 //   k_ed25519_sign        keygen + RFC 8032 signing (corpus generation / SignatureService
 //                         batch form; crypto/src/lib.rs:163-191) -- not constant time
 //   k_wcomb_bases/fill    wide-comb construction (B once per device, committee keys)
@@ -186,6 +187,21 @@ __global__ void k_wcomb_fill(const uint32_t* __restrict__ bases, uint32_t nkeys,
 // --------------------------------------------------------------------------
 // Certificate groups: AND of the per-signature bits in [first, first + cnt)
 // --------------------------------------------------------------------------
+// Per-signature message slices of certificate groups (message g = 32 bytes at
+// 32 g): the host entry points send first/cnt per group instead of 16 bytes of
+// offset/length per signature over PCIe.
+__global__ __launch_bounds__(kBlock) void k_group_msgs(const uint64_t* __restrict__ first,
+                                                      const uint32_t* __restrict__ cnt, uint64_t G,
+                                                      uint64_t* __restrict__ off, uint64_t* __restrict__ len) {
+  const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (g >= G) return;
+  const uint64_t f = first[g], c = cnt[g];
+  for (uint64_t q = 0; q < c; ++q) {
+    off[f + q] = 32 * g;
+    len[f + q] = 32;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_group_and(const uint64_t* __restrict__ first,
                                                      const uint32_t* __restrict__ cnt, uint64_t G,
                                                      const unsigned long long* __restrict__ sig_bits,
@@ -278,8 +294,7 @@ hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, co
                          const uint32_t* d_combB, void* d_ws, uint32_t ws_slots, uint64_t* d_out_words,
                          hipStream_t s) {
   if (n == 0) return hipSuccess;
-  uint64_t blocks = (n + 2 * kBlock - 1) / (2 * kBlock);  // two signatures per lane
-  if (blocks > ws_slots) blocks = ws_slots;
+  const uint64_t blocks = verify_grid(n, ws_slots);
   return mode == kStrict
              ? launch_verify_m<kStrict>(blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_combB, d_ws, d_out_words, s)
              : launch_verify_m<kCofactorless>(blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_combB, d_ws,
@@ -292,6 +307,14 @@ hipError_t launch_group_and(const uint64_t* d_first, const uint32_t* d_cnt, uint
   const uint64_t blocks = (G + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_group_and, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_first, d_cnt, G,
                      (const unsigned long long*)d_sig_words, (unsigned long long*)d_group_words);
+  return hipGetLastError();
+}
+
+hipError_t launch_group_msgs(const uint64_t* d_first, const uint32_t* d_cnt, uint64_t G, uint64_t* d_off,
+                             uint64_t* d_len, hipStream_t s) {
+  if (G == 0) return hipSuccess;
+  const uint64_t blocks = (G + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_group_msgs, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_first, d_cnt, G, d_off, d_len);
   return hipGetLastError();
 }
 
@@ -355,6 +378,16 @@ hipError_t launch_verify_keyset(int mode, const uint32_t* d_key_idx, const uint8
 size_t wcomb_bytes_per_key() { return kWWordsPerKey * 4; }
 size_t wcomb_bases_bytes_per_key() { return (size_t)kWPos * 40 * 4; }
 size_t wcomb_fill_tmp_bytes_per_key() { return (size_t)kWPos * kWChunks * kWChunk * 10 * 4; }
+// verify grid: one 512-signature block per workspace slot, at most ws_slots
+uint64_t verify_grid(uint64_t n, uint32_t ws_slots) {
+  const uint64_t blocks = (n + 2 * kBlock - 1) / (2 * kBlock);  // two signatures per lane
+  return blocks < ws_slots ? blocks : ws_slots;
+}
+
+// signatures one wave of resident workgroups covers (every CU full at the
+// kernel's occupancy): launches sized in whole rounds leave no partial last wave
+uint64_t keyset_round_sigs(uint32_t cus) { return (uint64_t)cus * 4 * keyset_occ() * 64 * kKsPerLane; }
+uint64_t verify_round_sigs(uint32_t cus) { return (uint64_t)cus * verify_occupancy() * 2 * kBlock; }
 uint64_t keyset_blocks(uint64_t n) { return (n + kKsPerLane * kBlock - 1) / (kKsPerLane * kBlock); }
 // stash of one launch (<= kKsMaxPerLaunch signatures: 1.25 GiB at most)
 size_t keyset_stash_bytes(uint64_t n) {

@@ -14,6 +14,9 @@ hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, co
                          hipStream_t s);
 hipError_t launch_group_and(const uint64_t* d_first, const uint32_t* d_cnt, uint64_t G,
                             const uint64_t* d_sig_words, uint64_t* d_group_words, hipStream_t s);
+// off[first[g] + q] = 32 g, len = 32 for q < cnt[g] (groups' 32-byte messages)
+hipError_t launch_group_msgs(const uint64_t* d_first, const uint32_t* d_cnt, uint64_t G, uint64_t* d_off,
+                             uint64_t* d_len, hipStream_t s);
 hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, const uint64_t* d_off,
                        const uint64_t* d_len, uint64_t n, const uint32_t* d_combB, uint8_t* d_pk,
                        uint8_t* d_sig, uint32_t max_blocks, hipStream_t s);
@@ -26,6 +29,9 @@ hipError_t launch_verify_keyset(int mode, const uint32_t* d_key_idx, const uint8
                                 const uint32_t* d_combB, void* d_stash, uint64_t* d_out_words, hipStream_t s);
 // key-cache verification: blocks of a launch over n signatures and the per-lane
 // stash it needs (d_stash above)
+uint64_t keyset_round_sigs(uint32_t cus);
+uint64_t verify_grid(uint64_t n, uint32_t ws_slots);  // blocks of a launch_verify
+uint64_t verify_round_sigs(uint32_t cus);
 uint64_t keyset_blocks(uint64_t n);
 size_t keyset_stash_bytes(uint64_t n);
 size_t wcomb_bytes_per_key();

@@ -79,7 +79,18 @@ struct Device {
   void* d_ws = nullptr;
   uint32_t ws_slots = 0;
   uint32_t sign_blocks = 0;
+  uint32_t cus = 0;
   hipEvent_t ws_done = nullptr;  // orders every kernel that uses d_ws, whatever its stream
+  // host entry points: chunk c's H2D copies go on cstream and chunk c's kernels
+  // wait for cev[c] on `stream`, so copies of chunk c+1 overlap kernels of chunk c
+  hipStream_t cstream = nullptr;
+  hipEvent_t cev[16] = {};
+  // ... and chunks alternate between two compute streams, so the waves of chunk
+  // c+1 fill the CUs that chunk c's last waves leave idle.  Stream 2 has its own
+  // verify workspace and key-cache stash.
+  hipStream_t stream2 = nullptr;
+  hipEvent_t join2 = nullptr, ws2_done = nullptr;
+  DevBuf ws2, stash2;
   std::mutex mu;
   DevBuf d[B_NBUF];
   HostBuf h[B_NBUF];
@@ -95,6 +106,15 @@ struct Device {
     if (d_combB) (void)hipFree(d_combB);
     if (d_ws) (void)hipFree(d_ws);
     if (ws_done) (void)hipEventDestroy(ws_done);
+    for (auto& e : cev)
+      if (e) (void)hipEventDestroy(e);
+    if (stream2) (void)hipStreamSynchronize(stream2);
+    if (ws2.p) (void)hipFree(ws2.p);
+    if (stash2.p) (void)hipFree(stash2.p);
+    if (join2) (void)hipEventDestroy(join2);
+    if (ws2_done) (void)hipEventDestroy(ws2_done);
+    if (stream2) (void)hipStreamDestroy(stream2);
+    if (cstream) (void)hipStreamDestroy(cstream);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -106,6 +126,11 @@ struct Device {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NT_ENODEV;
     NT_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     NT_TRY(hipEventCreateWithFlags(&ws_done, hipEventDisableTiming));
+    NT_TRY(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+    for (auto& e : cev) NT_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    NT_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+    NT_TRY(hipEventCreateWithFlags(&join2, hipEventDisableTiming));
+    NT_TRY(hipEventCreateWithFlags(&ws2_done, hipEventDisableTiming));
     {
       static const uint32_t kB[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                                      0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
@@ -121,6 +146,7 @@ struct Device {
     if (const char* e = std::getenv("NT_WS_SLOTS")) slots = (uint32_t)std::max(1, std::atoi(e));
     ws_slots = slots;
     sign_blocks = (uint32_t)prop.multiProcessorCount * 8;
+    cus = (uint32_t)prop.multiProcessorCount;
     if (hipMalloc(&d_ws, nt::ws_bytes_per_slot() * ws_slots) != hipSuccess) return NT_ENOMEM;
     NT_TRY(hipEventRecord(ws_done, stream));
     NT_TRY(hipStreamSynchronize(stream));
@@ -148,6 +174,39 @@ struct Device {
     if (d_bases) (void)hipFree(d_bases);
     if (d_tmp) (void)hipFree(d_tmp);
     return rc;
+  }
+
+  // compute stream of chunk c
+  hipStream_t cstr(int c) const { return (c & 1) ? stream2 : stream; }
+
+  // the kernels of chunk c wait for the copies issued so far on cstream
+  hipError_t fence(int c) {
+    hipError_t e = hipEventRecord(cev[c], cstream);
+    if (e != hipSuccess) return e;
+    return hipStreamWaitEvent(cstr(c), cev[c], 0);
+  }
+
+  // `stream` waits for everything issued on stream2
+  hipError_t join() {
+    hipError_t e = hipEventRecord(join2, stream2);
+    if (e != hipSuccess) return e;
+    return hipStreamWaitEvent(stream, join2, 0);
+  }
+
+  // verify launch of chunk c: even chunks use the device workspace on `stream`,
+  // odd chunks stream2's own workspace (grown to the chunk's grid)
+  int verify_chunk(int c, int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                   const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out) {
+    if (!(c & 1)) return verify(mode, pk, sig, msg, off, len, n, out, stream) == hipSuccess ? NT_OK : NT_EHIP;
+    const uint64_t blocks = nt::verify_grid(n, ws_slots);
+    const int rc = ws2.ensure(nt::ws_bytes_per_slot() * std::max<uint64_t>(blocks, 1));
+    if (rc != NT_OK) return rc;
+    if (hipStreamWaitEvent(stream2, ws2_done, 0) != hipSuccess ||
+        nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, ws2.p, (uint32_t)std::max<uint64_t>(blocks, 1),
+                          out, stream2) != hipSuccess ||
+        hipEventRecord(ws2_done, stream2) != hipSuccess)
+      return NT_EHIP;
+    return NT_OK;
   }
 
   // verify launch that shares the workspace: wait for the previous user, then mark
@@ -342,6 +401,158 @@ void words_to_bitmap(uint8_t* out, const uint64_t* words, uint64_t nbits) {
   if (nbits & 7) out[nbytes - 1] &= (uint8_t)((1u << (nbits & 7)) - 1);
 }
 
+// ---- chunked staging of the host entry points ----------------------------
+// A shard's items are split into up to kMaxChunks contiguous chunks (multiples
+// of 64 items, so each chunk owns whole 64-bit verdict words).  Chunk c's inputs
+// are copied on the copy stream, and its kernels wait only for those copies:
+// the PCIe transfer of chunk c+1 runs under the kernels of chunk c instead of
+// before all of them.  NT_PIPE_CHUNKS caps the count (1 = one copy, one launch;
+// default kMaxChunks).
+constexpr int kMaxChunks = 16;
+
+int pipe_chunks_cap() {
+  const char* e = std::getenv("NT_PIPE_CHUNKS");
+  const int v = e ? std::atoi(e) : kMaxChunks;
+  return std::max(1, std::min(kMaxChunks, v));
+}
+
+// NT_PIPE_ROUND overrides the round size (tests use it to split small inputs)
+uint64_t pipe_round(uint64_t R) {
+  const char* e = std::getenv("NT_PIPE_ROUND");
+  if (!e) return R;
+  const uint64_t v = (uint64_t)std::max(64ll, std::atoll(e));
+  return (v + 63) / 64 * 64;
+}
+
+// [0, m) -> chunks with the chunk_targets sizes (R a multiple of 64, so every
+// boundary is too: each chunk owns whole 64-bit verdict words)
+std::vector<uint64_t> chunk_targets(uint64_t total, uint64_t R);
+std::vector<std::pair<uint64_t, uint64_t>> plan_chunks(uint64_t m, uint64_t R) {
+  std::vector<std::pair<uint64_t, uint64_t>> r;
+  uint64_t a = 0;
+  for (uint64_t t : chunk_targets(m, R)) {
+    r.emplace_back(a, a + t);
+    a += t;
+  }
+  return r;
+}
+
+// Message bytes of items [lo, hi): the device buffer mirrors the host span
+// [base, base + span) (16-B phase kept); chunk c copies just the bytes its items
+// use, unless the items are not laid out in order, in which case chunk 0 copies
+// the whole span once.
+struct MsgStage {
+  uint64_t base = 0, span = 0;
+  bool whole = false;
+  std::vector<std::pair<uint64_t, uint64_t>> piece;  // per chunk [mn, mx), host-absolute
+};
+
+int msg_prepare(Device& dv, const uint64_t* off, const uint64_t* len, uint64_t lo,
+                const std::vector<std::pair<uint64_t, uint64_t>>& ch, MsgStage& ms) {
+  uint64_t gmn = UINT64_MAX, gmx = 0, sum = 0;
+  ms.piece.clear();
+  for (const auto& c : ch) {
+    uint64_t mn = UINT64_MAX, mx = 0;
+    for (uint64_t i = lo + c.first; i < lo + c.second; ++i) {
+      if (len[i] == 0) continue;
+      mn = std::min(mn, off[i]);
+      mx = std::max(mx, off[i] + len[i]);
+    }
+    if (mn == UINT64_MAX) mn = mx = 0;
+    ms.piece.emplace_back(mn, mx);
+    sum += mx - mn;
+    if (mx > mn) {
+      gmn = std::min(gmn, mn);
+      gmx = std::max(gmx, mx);
+    }
+  }
+  if (gmn == UINT64_MAX) gmn = gmx = 0;
+  ms.base = gmn & ~(uint64_t)15;
+  ms.span = gmx - ms.base;
+  ms.whole = sum > ms.span + ms.span / 4 + 4096;
+  const uint64_t m = ch.back().second;
+  NT_CHK(dv.d[B_DATA].ensure(ms.span + 64));
+  NT_CHK(dv.d[B_OFF].ensure(std::max<uint64_t>(m, 1) * 8));
+  NT_CHK(dv.d[B_LEN].ensure(std::max<uint64_t>(m, 1) * 8));
+  NT_CHK(dv.h[B_OFF].ensure(std::max<uint64_t>(m, 1) * 8));
+  NT_CHK(dv.h[B_LEN].ensure(std::max<uint64_t>(m, 1) * 8));
+  return NT_OK;
+}
+
+// copies (copy stream) of chunk c = items [lo + a, lo + b): rebased offsets,
+// lengths, and the chunk's message bytes
+int msg_copy(Device& dv, const uint8_t* data, const uint64_t* off, const uint64_t* len, uint64_t lo,
+             const MsgStage& ms, size_t c, uint64_t a, uint64_t b) {
+  uint64_t* ho = dv.h[B_OFF].as<uint64_t>();
+  uint64_t* hl = dv.h[B_LEN].as<uint64_t>();
+  for (uint64_t i = a; i < b; ++i) {
+    ho[i] = len[lo + i] ? off[lo + i] - ms.base : 0;
+    hl[i] = len[lo + i];
+  }
+  const auto& pc = ms.piece[c];
+  if (ms.whole) {
+    if (c == 0 && ms.span)
+      NT_TRY(hipMemcpyAsync(dv.d[B_DATA].p, data + ms.base, ms.span, hipMemcpyHostToDevice, dv.cstream));
+  } else if (pc.second > pc.first) {
+    NT_TRY(hipMemcpyAsync(dv.d[B_DATA].as<uint8_t>() + (pc.first - ms.base), data + pc.first, pc.second - pc.first,
+                          hipMemcpyHostToDevice, dv.cstream));
+  }
+  if (b > a) {
+    NT_TRY(hipMemcpyAsync(dv.d[B_OFF].as<uint64_t>() + a, ho + a, (b - a) * 8, hipMemcpyHostToDevice, dv.cstream));
+    NT_TRY(hipMemcpyAsync(dv.d[B_LEN].as<uint64_t>() + a, hl + a, (b - a) * 8, hipMemcpyHostToDevice, dv.cstream));
+  }
+  return NT_OK;
+}
+
+// Item counts per chunk in whole rounds R (the signatures one round of resident
+// waves covers, so no launch ends on a nearly empty round): a one-round first
+// chunk so the kernels start after a short copy, then equal whole-round chunks,
+// the last one takes the rest.
+std::vector<uint64_t> chunk_targets(uint64_t total, uint64_t R) {
+  const uint64_t cap = (uint64_t)pipe_chunks_cap();
+  if (cap == 1 || total <= R) return {total};
+  const uint64_t k = std::min<uint64_t>(cap, (total + R - 1) / R);
+  const uint64_t mid = ((total - R + k - 2) / (k - 1) + R - 1) / R * R;
+  std::vector<uint64_t> t{R};
+  uint64_t left = total - R;
+  while (left > mid) {
+    t.push_back(mid);
+    left -= mid;
+  }
+  t.push_back(left);
+  return t;
+}
+
+// Certificate groups [glo, ghi) -> chunks [g0, g1) holding about targets[c]
+// signatures each (at most that many when a boundary allows), every g0 - glo
+// a multiple of 64 (whole group-verdict words).
+std::vector<std::pair<uint64_t, uint64_t>> plan_group_chunks(uint64_t glo, uint64_t ghi, const uint32_t* cnt,
+                                                             const std::vector<uint64_t>& targets) {
+  std::vector<std::pair<uint64_t, uint64_t>> r;
+  uint64_t g0 = glo, acc = 0, cut = 0, acc_cut = 0;
+  size_t ti = 0;
+  for (uint64_t g = glo; g < ghi && ti + 1 < targets.size(); ++g) {
+    acc += cnt[g];
+    const uint64_t next = g + 1;
+    if ((next - glo) % 64 != 0 || next >= ghi) continue;
+    if (acc <= targets[ti]) {
+      cut = next;
+      acc_cut = acc;
+      if (acc < targets[ti]) continue;
+    } else if (cut == 0) {
+      cut = next;
+      acc_cut = acc;
+    }
+    r.emplace_back(g0, cut);
+    g0 = cut;
+    acc -= acc_cut;
+    cut = acc_cut = 0;
+    ++ti;
+  }
+  r.emplace_back(g0, ghi);
+  return r;
+}
+
 Device* dev_of(nt_ctx* ctx, int dev) {
   if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return nullptr;
   return ctx->devs[dev].get();
@@ -356,13 +567,21 @@ int nt_sha512_trunc32(nt_ctx* ctx, const uint8_t* data, const uint64_t* off, con
   if (!ctx || (n && (!off || !len || !out32))) return NT_EINVAL;
   if (n == 0) return NT_OK;
   return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
-    uint64_t base;
-    NT_CHK(stage_messages(dv, data, off, len, lo, hi, &base));
     const uint64_t m = hi - lo;
+    // a launch's time is set by its longest message: chunks of >= 64k messages
+    const auto ch = plan_chunks(m, pipe_round(1 << 16));
+    MsgStage ms;
+    NT_CHK(msg_prepare(dv, off, len, lo, ch, ms));
     NT_CHK(dv.d[B_OUT].ensure(m * 32));
-    NT_TRY(nt::launch_sha512_trunc32(dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>(),
-                                     dv.d[B_LEN].as<uint64_t>(), m, dv.d[B_OUT].as<uint8_t>(),
-                                     dv.stream));
+    for (size_t c = 0; c < ch.size(); ++c) {
+      const uint64_t a = ch[c].first, b = ch[c].second;
+      NT_CHK(msg_copy(dv, data, off, len, lo, ms, c, a, b));
+      NT_TRY(dv.fence((int)c));
+      NT_TRY(nt::launch_sha512_trunc32(dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>() + a,
+                                       dv.d[B_LEN].as<uint64_t>() + a, b - a, dv.d[B_OUT].as<uint8_t>() + 32 * a,
+                                       dv.cstr((int)c)));
+    }
+    NT_TRY(dv.join());
     NT_TRY(hipMemcpyAsync(out32 + 32 * lo, dv.d[B_OUT].p, m * 32, hipMemcpyDeviceToHost, dv.stream));
     NT_TRY(hipStreamSynchronize(dv.stream));
     return NT_OK;
@@ -375,18 +594,28 @@ int nt_ed25519_verify_strict(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* si
   if (!ctx || (n && (!pk32 || !sig64 || !off || !len || !out_bitmap))) return NT_EINVAL;
   if (n == 0) return NT_OK;
   return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
-    uint64_t base;
-    NT_CHK(stage_messages(dv, msg, off, len, lo, hi, &base));
     const uint64_t m = hi - lo, words = (m + 63) / 64;
+    const auto ch = plan_chunks(m, pipe_round(nt::verify_round_sigs(dv.cus)));
+    MsgStage ms;
+    NT_CHK(msg_prepare(dv, off, len, lo, ch, ms));
     NT_CHK(dv.d[B_PK].ensure(m * 32));
     NT_CHK(dv.d[B_SIG].ensure(m * 64));
     NT_CHK(dv.d[B_OUT].ensure(words * 8));
     NT_CHK(dv.h[B_OUT].ensure(words * 8));
-    NT_TRY(hipMemcpyAsync(dv.d[B_PK].p, pk32 + 32 * lo, m * 32, hipMemcpyHostToDevice, dv.stream));
-    NT_TRY(hipMemcpyAsync(dv.d[B_SIG].p, sig64 + 64 * lo, m * 64, hipMemcpyHostToDevice, dv.stream));
-    NT_TRY(dv.verify(NT_MODE_STRICT, dv.d[B_PK].as<uint8_t>(), dv.d[B_SIG].as<uint8_t>(),
-                     dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>(),
-                     dv.d[B_LEN].as<uint64_t>(), m, dv.d[B_OUT].as<uint64_t>(), dv.stream));
+    for (size_t c = 0; c < ch.size(); ++c) {
+      const uint64_t a = ch[c].first, b = ch[c].second;
+      NT_CHK(msg_copy(dv, msg, off, len, lo, ms, c, a, b));
+      NT_TRY(hipMemcpyAsync(dv.d[B_PK].as<uint8_t>() + 32 * a, pk32 + 32 * (lo + a), (b - a) * 32,
+                            hipMemcpyHostToDevice, dv.cstream));
+      NT_TRY(hipMemcpyAsync(dv.d[B_SIG].as<uint8_t>() + 64 * a, sig64 + 64 * (lo + a), (b - a) * 64,
+                            hipMemcpyHostToDevice, dv.cstream));
+      NT_TRY(dv.fence((int)c));
+      NT_CHK(dv.verify_chunk((int)c, NT_MODE_STRICT, dv.d[B_PK].as<uint8_t>() + 32 * a,
+                             dv.d[B_SIG].as<uint8_t>() + 64 * a, dv.d[B_DATA].as<uint8_t>(),
+                             dv.d[B_OFF].as<uint64_t>() + a, dv.d[B_LEN].as<uint64_t>() + a, b - a,
+                             dv.d[B_OUT].as<uint64_t>() + a / 64));
+    }
+    NT_TRY(dv.join());
     NT_TRY(hipMemcpyAsync(dv.h[B_OUT].p, dv.d[B_OUT].p, words * 8, hipMemcpyDeviceToHost, dv.stream));
     NT_TRY(hipStreamSynchronize(dv.stream));
     words_to_bitmap(out_bitmap + lo / 8, dv.h[B_OUT].as<uint64_t>(), m);
@@ -400,8 +629,8 @@ int nt_ed25519_verify_strict(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* si
 // compacted first / cnt.  Copies are split over host threads by signature count
 // (a config-3 batch stages ~0.6 GB; one thread would take ~50 ms of it).
 static void stage_groups(uint64_t glo, uint64_t ghi, const uint64_t* first, const uint32_t* cnt, size_t kw,
-                         const uint8_t* keys, const uint8_t* sig64, uint8_t* hkey, uint8_t* hsig, uint64_t* hoff,
-                         uint64_t* hlen, uint64_t* hfirst, uint32_t* hcnt) {
+                         const uint8_t* keys, const uint8_t* sig64, uint8_t* hkey, uint8_t* hsig, uint64_t* hfirst,
+                         uint32_t* hcnt) {
   uint64_t e = 0;
   for (uint64_t g = glo; g < ghi; ++g) {
     hfirst[g - glo] = e;
@@ -420,10 +649,6 @@ static void stage_groups(uint64_t glo, uint64_t ghi, const uint64_t* first, cons
       if (!c) continue;
       std::memcpy(hkey + kw * e0, keys + kw * first[g], kw * c);
       std::memcpy(hsig + 64 * e0, sig64 + 64 * first[g], 64 * c);
-      for (uint64_t q = 0; q < c; ++q) {
-        hoff[e0 + q] = 32 * (g - glo);
-        hlen[e0 + q] = 32;
-      }
     }
   };
   if (T == 1) {
@@ -436,39 +661,53 @@ static void stage_groups(uint64_t glo, uint64_t ghi, const uint64_t* first, cons
   for (auto& x : th) x.join();
 }
 
-int nt_ed25519_verify_batch_groups(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* sig64,
-                                   const uint64_t* first, const uint32_t* cnt,
-                                   const uint8_t* msg32, uint64_t G, uint8_t* out_group_bitmap,
-                                   uint8_t* out_sig_bitmap) {
-  if (!ctx || (G && (!first || !cnt || !msg32 || !out_group_bitmap))) return NT_EINVAL;
-  if (G == 0) return NT_OK;
+}  // extern "C"
+
+namespace {
+
+int dev_index(nt_ctx* ctx, const Device& dv) {
+  for (size_t i = 0; i < ctx->devs.size(); ++i)
+    if (ctx->devs[i].get() == &dv) return (int)i;
+  return -1;
+}
+
+// Certificate groups through either key form: ks == nullptr -> kw = 32-byte
+// encodings (verify kernel, cofactorless), else kw = 4-byte committee indices
+// (key-cache kernel).  Per shard, groups are staged chunk by chunk into pinned
+// memory (host threads) and copied on the copy stream; chunk c's verify and
+// group-AND launches wait only for chunk c's copies.
+int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* keys, const uint8_t* sig64,
+                  const uint64_t* first, const uint32_t* cnt, const uint8_t* msg32, uint64_t G,
+                  uint8_t* out_group_bitmap, uint8_t* out_sig_bitmap) {
   uint64_t nsig_total = 0;
   for (uint64_t g = 0; g < G; ++g) nsig_total = std::max(nsig_total, first[g] + cnt[g]);
-  if (nsig_total && (!pk32 || !sig64)) return NT_EINVAL;
+  if (nsig_total && (!keys || !sig64)) return NT_EINVAL;
   if (out_sig_bitmap) std::memset(out_sig_bitmap, 0, (nsig_total + 7) / 8);
   std::mutex sig_mu;
   return run_sharded(ctx, G, 64, [&](Device& dv, uint64_t glo, uint64_t ghi) -> int {
     const uint64_t gm = ghi - glo;
     uint64_t m = 0;
     for (uint64_t g = glo; g < ghi; ++g) m += cnt[g];
-    const uint64_t sw = (m + 63) / 64, gw = (gm + 63) / 64;
+    const uint64_t R = pipe_round(ks ? nt::keyset_round_sigs(dv.cus) : nt::verify_round_sigs(dv.cus));
+    const auto ch = plan_group_chunks(glo, ghi, cnt, chunk_targets(m, R));
+    const size_t C = ch.size();
+    // per chunk: first compacted signature, signature count, verdict-word base
+    std::vector<uint64_t> E(C + 1, 0), W(C + 1, 0);
+    for (size_t c = 0; c < C; ++c) {
+      uint64_t mc = 0;
+      for (uint64_t g = ch[c].first; g < ch[c].second; ++g) mc += cnt[g];
+      E[c + 1] = E[c] + mc;
+      W[c + 1] = W[c] + (mc + 63) / 64;
+    }
+    const uint64_t sw = W[C], gw = (gm + 63) / 64;
     const uint64_t mm = std::max<uint64_t>(m, 1);
-    NT_CHK(dv.h[B_PK].ensure(mm * 32));
+    NT_CHK(dv.h[B_PK].ensure(mm * kw));
     NT_CHK(dv.h[B_SIG].ensure(mm * 64));
-    NT_CHK(dv.h[B_OFF].ensure(mm * 8));
-    NT_CHK(dv.h[B_LEN].ensure(mm * 8));
     NT_CHK(dv.h[B_FIRST].ensure(gm * 8));
     NT_CHK(dv.h[B_CNT].ensure(gm * 4));
     NT_CHK(dv.h[B_OUT].ensure(sw * 8 + 8));
     NT_CHK(dv.h[B_OUT2].ensure(gw * 8));
-    uint8_t* hpk = dv.h[B_PK].as<uint8_t>();
-    uint8_t* hsig = dv.h[B_SIG].as<uint8_t>();
-    uint64_t* hoff = dv.h[B_OFF].as<uint64_t>();
-    uint64_t* hlen = dv.h[B_LEN].as<uint64_t>();
-    uint64_t* hfirst = dv.h[B_FIRST].as<uint64_t>();
-    uint32_t* hcnt = dv.h[B_CNT].as<uint32_t>();
-    stage_groups(glo, ghi, first, cnt, 32, pk32, sig64, hpk, hsig, hoff, hlen, hfirst, hcnt);
-    NT_CHK(dv.d[B_PK].ensure(mm * 32));
+    NT_CHK(dv.d[B_PK].ensure(mm * kw));
     NT_CHK(dv.d[B_SIG].ensure(mm * 64));
     NT_CHK(dv.d[B_OFF].ensure(mm * 8));
     NT_CHK(dv.d[B_LEN].ensure(mm * 8));
@@ -477,22 +716,57 @@ int nt_ed25519_verify_batch_groups(nt_ctx* ctx, const uint8_t* pk32, const uint8
     NT_CHK(dv.d[B_CNT].ensure(gm * 4));
     NT_CHK(dv.d[B_OUT].ensure(sw * 8 + 8));
     NT_CHK(dv.d[B_OUT2].ensure(gw * 8));
-    hipStream_t s = dv.stream;
-    if (m) {
-      NT_TRY(hipMemcpyAsync(dv.d[B_PK].p, hpk, m * 32, hipMemcpyHostToDevice, s));
-      NT_TRY(hipMemcpyAsync(dv.d[B_SIG].p, hsig, m * 64, hipMemcpyHostToDevice, s));
-      NT_TRY(hipMemcpyAsync(dv.d[B_OFF].p, hoff, m * 8, hipMemcpyHostToDevice, s));
-      NT_TRY(hipMemcpyAsync(dv.d[B_LEN].p, hlen, m * 8, hipMemcpyHostToDevice, s));
+    const void* pd_meta = nullptr;
+    if (ks) {
+      uint64_t mc = 0;
+      for (size_t c = 0; c < C; ++c) mc = std::max(mc, E[c + 1] - E[c]);
+      NT_CHK(dv.d[B_STASH].ensure(nt::keyset_stash_bytes(mc)));
+      if (C > 1) NT_CHK(dv.stash2.ensure(nt::keyset_stash_bytes(mc)));
+      pd_meta = &ks->dev[dev_index(ctx, dv)];
     }
-    NT_TRY(hipMemcpyAsync(dv.d[B_DATA].p, msg32 + 32 * glo, gm * 32, hipMemcpyHostToDevice, s));
-    NT_TRY(hipMemcpyAsync(dv.d[B_FIRST].p, hfirst, gm * 8, hipMemcpyHostToDevice, s));
-    NT_TRY(hipMemcpyAsync(dv.d[B_CNT].p, hcnt, gm * 4, hipMemcpyHostToDevice, s));
-    NT_TRY(hipMemsetAsync(dv.d[B_OUT].p, 0, sw * 8 + 8, s));
-    NT_TRY(dv.verify(NT_MODE_COFACTORLESS, dv.d[B_PK].as<uint8_t>(), dv.d[B_SIG].as<uint8_t>(),
-                     dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>(),
-                     dv.d[B_LEN].as<uint64_t>(), m, dv.d[B_OUT].as<uint64_t>(), s));
-    NT_TRY(nt::launch_group_and(dv.d[B_FIRST].as<uint64_t>(), dv.d[B_CNT].as<uint32_t>(), gm,
-                                dv.d[B_OUT].as<uint64_t>(), dv.d[B_OUT2].as<uint64_t>(), s));
+    uint8_t* hkey = dv.h[B_PK].as<uint8_t>();
+    uint8_t* hsig = dv.h[B_SIG].as<uint8_t>();
+    uint64_t* hfirst = dv.h[B_FIRST].as<uint64_t>();
+    uint32_t* hcnt = dv.h[B_CNT].as<uint32_t>();
+    hipStream_t cs = dv.cstream;
+    NT_TRY(hipMemsetAsync(dv.d[B_OUT].p, 0, sw * 8 + 8, cs));  // before every fence
+    for (size_t c = 0; c < C; ++c) {
+      const uint64_t g0 = ch[c].first, g1 = ch[c].second, gl = g0 - glo, e0 = E[c], mc = E[c + 1] - E[c];
+      // chunk-local: hfirst relative to e0; message offsets 32 * (g - g0) made on the device
+      stage_groups(g0, g1, first, cnt, kw, keys, sig64, hkey + kw * e0, hsig + 64 * e0, hfirst + gl, hcnt + gl);
+      if (mc) {
+        NT_TRY(hipMemcpyAsync(dv.d[B_PK].as<uint8_t>() + kw * e0, hkey + kw * e0, mc * kw, hipMemcpyHostToDevice, cs));
+        NT_TRY(hipMemcpyAsync(dv.d[B_SIG].as<uint8_t>() + 64 * e0, hsig + 64 * e0, mc * 64, hipMemcpyHostToDevice, cs));
+      }
+      NT_TRY(hipMemcpyAsync(dv.d[B_DATA].as<uint8_t>() + 32 * gl, msg32 + 32 * g0, (g1 - g0) * 32,
+                            hipMemcpyHostToDevice, cs));
+      NT_TRY(hipMemcpyAsync(dv.d[B_FIRST].as<uint64_t>() + gl, hfirst + gl, (g1 - g0) * 8, hipMemcpyHostToDevice, cs));
+      NT_TRY(hipMemcpyAsync(dv.d[B_CNT].as<uint32_t>() + gl, hcnt + gl, (g1 - g0) * 4, hipMemcpyHostToDevice, cs));
+      NT_TRY(dv.fence((int)c));
+      hipStream_t s = dv.cstr((int)c);
+      const uint8_t* dk = dv.d[B_PK].as<uint8_t>() + kw * e0;
+      const uint8_t* dsig = dv.d[B_SIG].as<uint8_t>() + 64 * e0;
+      const uint8_t* dmsg = dv.d[B_DATA].as<uint8_t>() + 32 * gl;
+      const uint64_t* doff = dv.d[B_OFF].as<uint64_t>() + e0;
+      const uint64_t* dlen = dv.d[B_LEN].as<uint64_t>() + e0;
+      uint64_t* dout = dv.d[B_OUT].as<uint64_t>() + W[c];
+      if (mc) {
+        NT_TRY(nt::launch_group_msgs(dv.d[B_FIRST].as<uint64_t>() + gl, dv.d[B_CNT].as<uint32_t>() + gl, g1 - g0,
+                                     (uint64_t*)doff, (uint64_t*)dlen, s));
+        if (ks) {
+          const auto& pd = *(const nt_keyset::PerDev*)pd_meta;
+          NT_TRY(nt::launch_verify_keyset(NT_MODE_COFACTORLESS, (const uint32_t*)dk, dsig, dmsg, doff, dlen, mc,
+                                          pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB,
+                                          (c & 1) ? dv.stash2.p : dv.d[B_STASH].p, dout, s));
+        } else {
+          NT_CHK(dv.verify_chunk((int)c, NT_MODE_COFACTORLESS, dk, dsig, dmsg, doff, dlen, mc, dout));
+        }
+      }
+      NT_TRY(nt::launch_group_and(dv.d[B_FIRST].as<uint64_t>() + gl, dv.d[B_CNT].as<uint32_t>() + gl, g1 - g0, dout,
+                                  dv.d[B_OUT2].as<uint64_t>() + gl / 64, s));
+    }
+    hipStream_t s = dv.stream;
+    NT_TRY(dv.join());
     NT_TRY(hipMemcpyAsync(dv.h[B_OUT2].p, dv.d[B_OUT2].p, gw * 8, hipMemcpyDeviceToHost, s));
     if (out_sig_bitmap && m)
       NT_TRY(hipMemcpyAsync(dv.h[B_OUT].p, dv.d[B_OUT].p, sw * 8, hipMemcpyDeviceToHost, s));
@@ -501,18 +775,31 @@ int nt_ed25519_verify_batch_groups(nt_ctx* ctx, const uint8_t* pk32, const uint8
     if (out_sig_bitmap && m) {
       const uint64_t* bits = dv.h[B_OUT].as<uint64_t>();
       std::lock_guard<std::mutex> lk(sig_mu);
-      uint64_t e2 = 0;
-      for (uint64_t g = glo; g < ghi; ++g) {
-        for (uint32_t t = 0; t < cnt[g]; ++t, ++e2) {
-          if ((bits[e2 >> 6] >> (e2 & 63)) & 1) {
-            const uint64_t o = first[g] + t;
-            out_sig_bitmap[o >> 3] |= (uint8_t)(1u << (o & 7));
-          }
-        }
+      for (size_t c = 0; c < C; ++c) {
+        uint64_t e2 = 64 * W[c];
+        for (uint64_t g = ch[c].first; g < ch[c].second; ++g)
+          for (uint32_t t = 0; t < cnt[g]; ++t, ++e2)
+            if ((bits[e2 >> 6] >> (e2 & 63)) & 1) {
+              const uint64_t o = first[g] + t;
+              out_sig_bitmap[o >> 3] |= (uint8_t)(1u << (o & 7));
+            }
       }
     }
     return NT_OK;
   });
+}
+
+}  // namespace
+
+extern "C" {
+
+int nt_ed25519_verify_batch_groups(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* sig64,
+                                   const uint64_t* first, const uint32_t* cnt,
+                                   const uint8_t* msg32, uint64_t G, uint8_t* out_group_bitmap,
+                                   uint8_t* out_sig_bitmap) {
+  if (!ctx || (G && (!first || !cnt || !msg32 || !out_group_bitmap))) return NT_EINVAL;
+  if (G == 0) return NT_OK;
+  return verify_groups(ctx, nullptr, 32, pk32, sig64, first, cnt, msg32, G, out_group_bitmap, out_sig_bitmap);
 }
 
 int nt_ed25519_sign_batch(nt_ctx* ctx, const uint8_t* seed32, const uint8_t* msg,
@@ -592,11 +879,6 @@ int nt_keyset_flags(const nt_keyset* ks, uint32_t i, uint32_t* flags) {
   return NT_OK;
 }
 
-static int dev_index(nt_ctx* ctx, const Device& dv) {
-  for (size_t i = 0; i < ctx->devs.size(); ++i)
-    if (ctx->devs[i].get() == &dv) return (int)i;
-  return -1;
-}
 
 int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const uint32_t* key_idx,
                              const uint8_t* sig64, const uint8_t* msg, const uint64_t* off,
@@ -606,20 +888,33 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
   if (n == 0) return NT_OK;
   return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
     const auto& pd = ks->dev[dev_index(ctx, dv)];
-    uint64_t base;
-    NT_CHK(stage_messages(dv, msg, off, len, lo, hi, &base));
     const uint64_t m = hi - lo, words = (m + 63) / 64;
+    const auto ch = plan_chunks(m, pipe_round(nt::keyset_round_sigs(dv.cus)));
+    MsgStage ms;
+    NT_CHK(msg_prepare(dv, off, len, lo, ch, ms));
     NT_CHK(dv.d[B_PK].ensure(m * 4));
     NT_CHK(dv.d[B_SIG].ensure(m * 64));
     NT_CHK(dv.d[B_OUT].ensure(words * 8));
     NT_CHK(dv.h[B_OUT].ensure(words * 8));
-    NT_TRY(hipMemcpyAsync(dv.d[B_PK].p, key_idx + lo, m * 4, hipMemcpyHostToDevice, dv.stream));
-    NT_TRY(hipMemcpyAsync(dv.d[B_SIG].p, sig64 + 64 * lo, m * 64, hipMemcpyHostToDevice, dv.stream));
-    NT_CHK(dv.d[B_STASH].ensure(nt::keyset_stash_bytes(m)));
-    NT_TRY(nt::launch_verify_keyset(mode, dv.d[B_PK].as<uint32_t>(), dv.d[B_SIG].as<uint8_t>(),
-                                    dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>(),
-                                    dv.d[B_LEN].as<uint64_t>(), m, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys,
-                                    dv.d_combB, dv.d[B_STASH].p, dv.d[B_OUT].as<uint64_t>(), dv.stream));
+    uint64_t mc = 0;
+    for (const auto& c : ch) mc = std::max(mc, c.second - c.first);
+    NT_CHK(dv.d[B_STASH].ensure(nt::keyset_stash_bytes(mc)));
+    if (ch.size() > 1) NT_CHK(dv.stash2.ensure(nt::keyset_stash_bytes(mc)));
+    for (size_t c = 0; c < ch.size(); ++c) {
+      const uint64_t a = ch[c].first, b = ch[c].second;
+      NT_CHK(msg_copy(dv, msg, off, len, lo, ms, c, a, b));
+      NT_TRY(hipMemcpyAsync(dv.d[B_PK].as<uint32_t>() + a, key_idx + lo + a, (b - a) * 4, hipMemcpyHostToDevice,
+                            dv.cstream));
+      NT_TRY(hipMemcpyAsync(dv.d[B_SIG].as<uint8_t>() + 64 * a, sig64 + 64 * (lo + a), (b - a) * 64,
+                            hipMemcpyHostToDevice, dv.cstream));
+      NT_TRY(dv.fence((int)c));
+      NT_TRY(nt::launch_verify_keyset(mode, dv.d[B_PK].as<uint32_t>() + a, dv.d[B_SIG].as<uint8_t>() + 64 * a,
+                                      dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>() + a,
+                                      dv.d[B_LEN].as<uint64_t>() + a, b - a, pd.d_meta, pd.d_enc, pd.d_comb,
+                                      ks->nkeys, dv.d_combB, (c & 1) ? dv.stash2.p : dv.d[B_STASH].p,
+                                      dv.d[B_OUT].as<uint64_t>() + a / 64, dv.cstr((int)c)));
+    }
+    NT_TRY(dv.join());
     NT_TRY(hipMemcpyAsync(dv.h[B_OUT].p, dv.d[B_OUT].p, words * 8, hipMemcpyDeviceToHost, dv.stream));
     NT_TRY(hipStreamSynchronize(dv.stream));
     words_to_bitmap(out_bitmap + lo / 8, dv.h[B_OUT].as<uint64_t>(), m);
@@ -634,79 +929,8 @@ int nt_ed25519_verify_batch_groups_keyset(nt_ctx* ctx, const nt_keyset* ks, cons
   if (!ctx || !ks || ks->ctx != ctx) return NT_EINVAL;
   if (G && (!first || !cnt || !msg32 || !out_group_bitmap)) return NT_EINVAL;
   if (G == 0) return NT_OK;
-  uint64_t nsig_total = 0;
-  for (uint64_t g = 0; g < G; ++g) nsig_total = std::max(nsig_total, first[g] + cnt[g]);
-  if (nsig_total && (!key_idx || !sig64)) return NT_EINVAL;
-  if (out_sig_bitmap) std::memset(out_sig_bitmap, 0, (nsig_total + 7) / 8);
-  std::mutex sig_mu;
-  return run_sharded(ctx, G, 64, [&](Device& dv, uint64_t glo, uint64_t ghi) -> int {
-    const auto& pd = ks->dev[dev_index(ctx, dv)];
-    const uint64_t gm = ghi - glo;
-    uint64_t m = 0;
-    for (uint64_t g = glo; g < ghi; ++g) m += cnt[g];
-    const uint64_t sw = (m + 63) / 64, gw = (gm + 63) / 64;
-    const uint64_t mm = std::max<uint64_t>(m, 1);
-    NT_CHK(dv.h[B_PK].ensure(mm * 4));
-    NT_CHK(dv.h[B_SIG].ensure(mm * 64));
-    NT_CHK(dv.h[B_OFF].ensure(mm * 8));
-    NT_CHK(dv.h[B_LEN].ensure(mm * 8));
-    NT_CHK(dv.h[B_FIRST].ensure(gm * 8));
-    NT_CHK(dv.h[B_CNT].ensure(gm * 4));
-    NT_CHK(dv.h[B_OUT].ensure(sw * 8 + 8));
-    NT_CHK(dv.h[B_OUT2].ensure(gw * 8));
-    uint32_t* hki = dv.h[B_PK].as<uint32_t>();
-    uint8_t* hsig = dv.h[B_SIG].as<uint8_t>();
-    uint64_t* hoff = dv.h[B_OFF].as<uint64_t>();
-    uint64_t* hlen = dv.h[B_LEN].as<uint64_t>();
-    uint64_t* hfirst = dv.h[B_FIRST].as<uint64_t>();
-    uint32_t* hcnt = dv.h[B_CNT].as<uint32_t>();
-    stage_groups(glo, ghi, first, cnt, 4, (const uint8_t*)key_idx, sig64, (uint8_t*)hki, hsig, hoff, hlen, hfirst,
-                 hcnt);
-    NT_CHK(dv.d[B_PK].ensure(mm * 4));
-    NT_CHK(dv.d[B_SIG].ensure(mm * 64));
-    NT_CHK(dv.d[B_OFF].ensure(mm * 8));
-    NT_CHK(dv.d[B_LEN].ensure(mm * 8));
-    NT_CHK(dv.d[B_DATA].ensure(gm * 32 + 64));
-    NT_CHK(dv.d[B_FIRST].ensure(gm * 8));
-    NT_CHK(dv.d[B_CNT].ensure(gm * 4));
-    NT_CHK(dv.d[B_OUT].ensure(sw * 8 + 8));
-    NT_CHK(dv.d[B_OUT2].ensure(gw * 8));
-    hipStream_t s = dv.stream;
-    if (m) {
-      NT_TRY(hipMemcpyAsync(dv.d[B_PK].p, hki, m * 4, hipMemcpyHostToDevice, s));
-      NT_TRY(hipMemcpyAsync(dv.d[B_SIG].p, hsig, m * 64, hipMemcpyHostToDevice, s));
-      NT_TRY(hipMemcpyAsync(dv.d[B_OFF].p, hoff, m * 8, hipMemcpyHostToDevice, s));
-      NT_TRY(hipMemcpyAsync(dv.d[B_LEN].p, hlen, m * 8, hipMemcpyHostToDevice, s));
-    }
-    NT_TRY(hipMemcpyAsync(dv.d[B_DATA].p, msg32 + 32 * glo, gm * 32, hipMemcpyHostToDevice, s));
-    NT_TRY(hipMemcpyAsync(dv.d[B_FIRST].p, hfirst, gm * 8, hipMemcpyHostToDevice, s));
-    NT_TRY(hipMemcpyAsync(dv.d[B_CNT].p, hcnt, gm * 4, hipMemcpyHostToDevice, s));
-    NT_TRY(hipMemsetAsync(dv.d[B_OUT].p, 0, sw * 8 + 8, s));
-    NT_CHK(dv.d[B_STASH].ensure(nt::keyset_stash_bytes(m)));
-    NT_TRY(nt::launch_verify_keyset(NT_MODE_COFACTORLESS, dv.d[B_PK].as<uint32_t>(), dv.d[B_SIG].as<uint8_t>(),
-                                    dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>(),
-                                    dv.d[B_LEN].as<uint64_t>(), m, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys,
-                                    dv.d_combB, dv.d[B_STASH].p, dv.d[B_OUT].as<uint64_t>(), s));
-    NT_TRY(nt::launch_group_and(dv.d[B_FIRST].as<uint64_t>(), dv.d[B_CNT].as<uint32_t>(), gm,
-                                dv.d[B_OUT].as<uint64_t>(), dv.d[B_OUT2].as<uint64_t>(), s));
-    NT_TRY(hipMemcpyAsync(dv.h[B_OUT2].p, dv.d[B_OUT2].p, gw * 8, hipMemcpyDeviceToHost, s));
-    if (out_sig_bitmap && m)
-      NT_TRY(hipMemcpyAsync(dv.h[B_OUT].p, dv.d[B_OUT].p, sw * 8, hipMemcpyDeviceToHost, s));
-    NT_TRY(hipStreamSynchronize(s));
-    words_to_bitmap(out_group_bitmap + glo / 8, dv.h[B_OUT2].as<uint64_t>(), gm);
-    if (out_sig_bitmap && m) {
-      const uint64_t* bits = dv.h[B_OUT].as<uint64_t>();
-      std::lock_guard<std::mutex> lk(sig_mu);
-      uint64_t e2 = 0;
-      for (uint64_t g = glo; g < ghi; ++g)
-        for (uint32_t t = 0; t < cnt[g]; ++t, ++e2)
-          if ((bits[e2 >> 6] >> (e2 & 63)) & 1) {
-            const uint64_t o = first[g] + t;
-            out_sig_bitmap[o >> 3] |= (uint8_t)(1u << (o & 7));
-          }
-    }
-    return NT_OK;
-  });
+  return verify_groups(ctx, ks, 4, (const uint8_t*)key_idx, sig64, first, cnt, msg32, G, out_group_bitmap,
+                       out_sig_bitmap);
 }
 
 // ---- device-resident entry points ---------------------------------------

@@ -80,3 +80,106 @@ def test_keyset_launch_chunking(pair):
     got = ks.verify(0, key, sigs, msg, off, ln)
     ks.close()
     assert np.array_equal(got, expect)
+
+
+def test_concurrent_callers(pair):
+    """The ABI is re-entrant (the worker's two Processor tasks and
+    the primary's Core call it from different threads): six host threads issue
+    digests, strict verifies, batch groups and key-cache verifies through ONE
+    context at the same time; every result equals the single-threaded one."""
+    from concurrent.futures import ThreadPoolExecutor
+    one, three = pair
+    rng = np.random.default_rng(8)
+    n = 700
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    msgs = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in rng.integers(0, 300, n)]
+    data, off, ln = _pack(msgs)
+    pk, sig = one.sign_batch(seeds, data, off, ln)
+    sig = sig.copy()
+    sig[::7, 40] ^= 2
+    g = np.load(os.path.join(GOLD, "batch_groups.npz"))
+    uniq, inv = np.unique(g["pk"], axis=0, return_inverse=True)
+    inv = inv.astype(np.uint32).ravel()
+    want = {
+        "sha": one.sha512_trunc32(data, off, ln),
+        "strict": one.verify_strict(pk, sig, data, off, ln),
+        "groups": one.verify_batch_groups(g["pk"], g["sig"], g["first"], g["cnt"], g["msg32"]),
+    }
+    for be in (one, three):
+        ks = be.keyset(uniq)
+        want_ks = ks.verify_batch_groups(inv, g["sig"], g["first"], g["cnt"], g["msg32"])
+        calls = {
+            "sha": lambda: be.sha512_trunc32(data, off, ln),
+            "strict": lambda: be.verify_strict(pk, sig, data, off, ln),
+            "groups": lambda: be.verify_batch_groups(g["pk"], g["sig"], g["first"], g["cnt"], g["msg32"]),
+            "keyset": lambda: ks.verify_batch_groups(inv, g["sig"], g["first"], g["cnt"], g["msg32"]),
+        }
+        kinds = [k for _ in range(12) for k in calls]
+        with ThreadPoolExecutor(6) as ex:
+            outs = list(ex.map(lambda k: (k, calls[k]()), kinds))
+        for k, got in outs:
+            assert np.array_equal(got, want_ks if k == "keyset" else want[k]), k
+        ks.close()
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0]])
+def test_chunked_host_calls_match(devices, monkeypatch):
+    """The host entry points copy and launch chunk by chunk (copies of chunk c+1
+    under the kernels of chunk c).  NT_PIPE_ROUND shrinks the chunk unit so a
+    few thousand items split into many chunks: digests, strict / key-cache
+    verdicts and certificate-group verdicts (ragged groups, empty groups, group
+    counts not a multiple of 64, messages out of order) must equal the
+    single-chunk results bit for bit."""
+    import ntcrypto
+    be = ntcrypto.Backend(devices=devices)
+    rng = np.random.default_rng(99)
+    n = 3001
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    msgs = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in rng.integers(0, 260, n)]
+    data, off, ln = _pack(msgs)
+    pk, sig = be.sign_batch(seeds, data, off, ln)
+    sig = sig.copy()
+    bad = rng.choice(n, 40, replace=False)
+    sig[bad, 9] ^= 4
+    # a second layout: the same messages, stored in reverse order
+    perm = np.arange(n)[::-1]
+    data_r, off_r, ln_r = _pack([msgs[i] for i in perm])
+    off_rev = np.empty(n, np.uint64)
+    off_rev[perm] = off_r
+    # groups: ragged, some empty, votes drawn from a 50-key committee
+    kseeds = rng.integers(0, 256, (50, 32), dtype=np.uint8)
+    G = 203
+    cnt = rng.integers(0, 30, G).astype(np.uint32)
+    cnt[[3, 77]] = 0
+    first = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.uint64)
+    m = int(cnt.sum())
+    kidx = rng.integers(0, 50, m).astype(np.uint32)
+    msg32 = rng.integers(0, 256, (G, 32), dtype=np.uint8)
+    gmsg = np.repeat(msg32, cnt.astype(np.int64), axis=0).ravel()
+    goff, gln = np.arange(m, dtype=np.uint64) * 32, np.full(m, 32, np.uint64)
+    gpk, gsig = be.sign_batch(kseeds[kidx], gmsg, goff, gln)
+    gsig = gsig.copy()
+    gsig[rng.choice(m, 25, replace=False), 50] ^= 1
+    kpk = be.sign_batch(kseeds)
+    ks = be.keyset(kpk)
+
+    def run():
+        return [be.sha512_trunc32(data, off, ln), be.sha512_trunc32(data_r, off_rev, ln),
+                be.verify_strict(pk, sig, data, off, ln), be.verify_strict(pk, sig, data_r, off_rev, ln),
+                ks.verify(0, kidx, gsig, gmsg, goff, gln),
+                *be.verify_batch_groups(gpk, gsig, first, cnt, msg32, with_sig_bits=True),
+                *ks.verify_batch_groups(kidx, gsig, first, cnt, msg32, with_sig_bits=True)]
+
+    monkeypatch.setenv("NT_PIPE_CHUNKS", "1")
+    want = run()
+    assert not want[2][bad].any() and want[2].sum() == n - len(bad)
+    assert want[4].sum() == m - 25
+    assert want[5].sum() < G and want[5][[3, 77]].all()
+    for rnd in ("64", "640", "1000"):
+        monkeypatch.setenv("NT_PIPE_CHUNKS", "16")
+        monkeypatch.setenv("NT_PIPE_ROUND", rnd)
+        got = run()
+        for k, (a, b) in enumerate(zip(want, got)):
+            assert np.array_equal(a, b), (rnd, k)
+    ks.close()
+    be.close()
