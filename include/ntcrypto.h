@@ -121,6 +121,17 @@ int nt_ed25519_verify_batch_groups_keyset(nt_ctx *ctx, const nt_keyset *ks, cons
                                           const uint32_t *cnt, const uint8_t *msg32, uint64_t G,
                                           uint8_t *out_group_bitmap, uint8_t *out_sig_bitmap);
 
+/* ---- pinned host buffers ---------------------------------------------
+ * Page-locked host memory for callers that stage large batches themselves
+ * (the primary's wire ingestion).  Inputs that lie in such a buffer are
+ * copied to the device by DMA straight from it: the host entry points skip
+ * their own staging copy (for certificate groups: when the groups' signatures
+ * and keys are also densely packed, first[g + 1] == first[g] + cnt[g]).
+ * No reference counterpart: the reference's Rust callers own ordinary Vecs.
+ * Returns NULL when no device / no memory. */
+void *nt_host_alloc(uint64_t bytes);
+void nt_host_free(void *p);
+
 /* ---- device-resident entry points (enqueue only) ---------------------- */
 int nt_dev_sha512_trunc32(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_data,
                           const uint64_t *d_off, const uint64_t *d_len, uint64_t n,

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -69,6 +70,18 @@ struct HostBuf {
   template <class T>
   T* as() const { return (T*)p; }
 };
+
+// nt_host_alloc registry: [base, base + bytes) of every live pinned buffer
+std::mutex g_pin_mu;
+std::map<uintptr_t, uint64_t> g_pinned;
+
+bool is_pinned(const void* p, uint64_t bytes) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  auto it = g_pinned.upper_bound((uintptr_t)p);
+  if (it == g_pinned.begin()) return false;
+  --it;
+  return (uintptr_t)p + bytes <= it->first + it->second;
+}
 
 enum { B_DATA, B_OFF, B_LEN, B_PK, B_SIG, B_OUT, B_OUT2, B_FIRST, B_CNT, B_STASH, B_NBUF };
 
@@ -309,6 +322,23 @@ int nt_init_devices(nt_ctx** out, const int* ordinals, int n) {
 void nt_free(nt_ctx* ctx) { delete ctx; }
 
 int nt_num_devices(const nt_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+void* nt_host_alloc(uint64_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, std::max<uint64_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pinned[(uintptr_t)p] = std::max<uint64_t>(bytes, 1);
+  return p;
+}
+
+void nt_host_free(void* p) {
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    g_pinned.erase((uintptr_t)p);
+  }
+  (void)hipHostFree(p);
+}
 
 }  // extern "C"
 
@@ -630,7 +660,7 @@ int nt_ed25519_verify_strict(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* si
 // (a config-3 batch stages ~0.6 GB; one thread would take ~50 ms of it).
 static void stage_groups(uint64_t glo, uint64_t ghi, const uint64_t* first, const uint32_t* cnt, size_t kw,
                          const uint8_t* keys, const uint8_t* sig64, uint8_t* hkey, uint8_t* hsig, uint64_t* hfirst,
-                         uint32_t* hcnt) {
+                         uint32_t* hcnt, bool copy_data) {
   uint64_t e = 0;
   for (uint64_t g = glo; g < ghi; ++g) {
     hfirst[g - glo] = e;
@@ -638,6 +668,7 @@ static void stage_groups(uint64_t glo, uint64_t ghi, const uint64_t* first, cons
     e += cnt[g];
   }
   const uint64_t m = e;
+  if (!copy_data) return;
   const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   const unsigned T = m < (1u << 16) ? 1u : hw;
   auto work = [&](unsigned t) {
@@ -701,8 +732,12 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
     }
     const uint64_t sw = W[C], gw = (gm + 63) / 64;
     const uint64_t mm = std::max<uint64_t>(m, 1);
-    NT_CHK(dv.h[B_PK].ensure(mm * kw));
-    NT_CHK(dv.h[B_SIG].ensure(mm * 64));
+    // caller's keys and signatures already in nt_host_alloc memory and densely
+    // packed: DMA straight from them, no staging copy
+    bool direct = m > 0 && is_pinned(keys + kw * first[glo], kw * m) && is_pinned(sig64 + 64 * first[glo], 64 * m);
+    for (uint64_t g = glo; direct && g + 1 < ghi; ++g) direct = first[g + 1] == first[g] + cnt[g];
+    NT_CHK(dv.h[B_PK].ensure(direct ? 1 : mm * kw));
+    NT_CHK(dv.h[B_SIG].ensure(direct ? 1 : mm * 64));
     NT_CHK(dv.h[B_FIRST].ensure(gm * 8));
     NT_CHK(dv.h[B_CNT].ensure(gm * 4));
     NT_CHK(dv.h[B_OUT].ensure(sw * 8 + 8));
@@ -733,10 +768,13 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
     for (size_t c = 0; c < C; ++c) {
       const uint64_t g0 = ch[c].first, g1 = ch[c].second, gl = g0 - glo, e0 = E[c], mc = E[c + 1] - E[c];
       // chunk-local: hfirst relative to e0; message offsets 32 * (g - g0) made on the device
-      stage_groups(g0, g1, first, cnt, kw, keys, sig64, hkey + kw * e0, hsig + 64 * e0, hfirst + gl, hcnt + gl);
+      stage_groups(g0, g1, first, cnt, kw, keys, sig64, hkey + kw * e0, hsig + 64 * e0, hfirst + gl, hcnt + gl,
+                   !direct);
       if (mc) {
-        NT_TRY(hipMemcpyAsync(dv.d[B_PK].as<uint8_t>() + kw * e0, hkey + kw * e0, mc * kw, hipMemcpyHostToDevice, cs));
-        NT_TRY(hipMemcpyAsync(dv.d[B_SIG].as<uint8_t>() + 64 * e0, hsig + 64 * e0, mc * 64, hipMemcpyHostToDevice, cs));
+        const uint8_t* sk = direct ? keys + kw * (first[glo] + e0) : hkey + kw * e0;
+        const uint8_t* ss = direct ? sig64 + 64 * (first[glo] + e0) : hsig + 64 * e0;
+        NT_TRY(hipMemcpyAsync(dv.d[B_PK].as<uint8_t>() + kw * e0, sk, mc * kw, hipMemcpyHostToDevice, cs));
+        NT_TRY(hipMemcpyAsync(dv.d[B_SIG].as<uint8_t>() + 64 * e0, ss, mc * 64, hipMemcpyHostToDevice, cs));
       }
       NT_TRY(hipMemcpyAsync(dv.d[B_DATA].as<uint8_t>() + 32 * gl, msg32 + 32 * g0, (g1 - g0) * 32,
                             hipMemcpyHostToDevice, cs));

@@ -18,7 +18,6 @@
 #include <cstring>
 #include <string_view>
 #include <thread>
-#include <unordered_map>
 
 #include "../../include/ntcrypto.h"
 #include "narwhal.hpp"
@@ -34,17 +33,51 @@ struct KeyIndex {
   std::vector<PublicKey> keys;        // committee order (BTreeMap = byte order)
   std::vector<Stake> stake;
   std::vector<std::vector<WorkerId>> workers;
-  std::vector<std::string> b64;                          // canonical encodings
-  std::unordered_map<std::string_view, uint32_t> by_b64;  // views into b64
+  std::vector<std::string> b64;       // canonical encodings
   explicit KeyIndex(const Committee& c) {
-    b64.reserve(c.authorities.size());
     for (const auto& kv : c.authorities) {
       b64.push_back(kv.first.encode_base64());
-      by_b64.emplace(std::string_view(b64.back()), (uint32_t)keys.size());
       keys.push_back(kv.first);
       stake.push_back(kv.second.stake);
       workers.emplace_back(kv.second.workers.begin(), kv.second.workers.end());
     }
+    build_slots();
+  }
+  // Canonical encodings by their first 8 characters (open addressing; the other
+  // 36 are compared): one multiply, one probe and a 36-byte compare per key
+  // string instead of hashing all 44 bytes into an unordered_map.
+  static constexpr uint32_t kEmpty = 0xffffffffu;
+  std::vector<uint64_t> slot_head;
+  std::vector<uint32_t> slot_idx;
+  int slot_bits = 0;
+  static uint64_t head_of(const uint8_t* s) {
+    uint64_t h;
+    std::memcpy(&h, s, 8);
+    return h;
+  }
+  size_t slot_of(uint64_t h) const { return (size_t)((h * 0x9E3779B97F4A7C15ull) >> (64 - slot_bits)); }
+  void build_slots() {
+    slot_bits = 4;
+    while ((1ull << slot_bits) < 4 * b64.size()) ++slot_bits;
+    slot_head.assign(1ull << slot_bits, 0);
+    slot_idx.assign(1ull << slot_bits, kEmpty);
+    const size_t mask = (1ull << slot_bits) - 1;
+    for (uint32_t k = 0; k < b64.size(); ++k) {
+      const uint64_t h = head_of((const uint8_t*)b64[k].data());
+      size_t i = slot_of(h);
+      while (slot_idx[i] != kEmpty) i = (i + 1) & mask;
+      slot_head[i] = h;
+      slot_idx[i] = k;
+    }
+  }
+  // committee index of a canonical 44-character encoding, kEmpty otherwise
+  uint32_t find_b64(const uint8_t* s, size_t len) const {
+    if (len != 44) return kEmpty;
+    const uint64_t h = head_of(s);
+    const size_t mask = (1ull << slot_bits) - 1;
+    for (size_t i = slot_of(h); slot_idx[i] != kEmpty; i = (i + 1) & mask)
+      if (slot_head[i] == h && std::memcmp(b64[slot_idx[i]].data() + 8, s + 8, 36) == 0) return slot_idx[i];
+    return kEmpty;
   }
   uint32_t of_bytes(const PublicKey& pk) const {
     auto it = std::lower_bound(keys.begin(), keys.end(), pk);
@@ -61,14 +94,48 @@ struct Rec {
   PublicKey author_pk, origin_pk;             // raw keys (preimages, vote target check)
   std::array<uint8_t, 32> id{};
   std::array<uint8_t, 64> sig{};
-  uint64_t pre_off = 0, pre_len = 0;          // header preimage in the thread arena
+  const uint8_t* pay = nullptr;               // header payload entries (36 B each) in the wire
+  const uint8_t* par = nullptr;               // header parents (32 B each) in the wire
+  uint64_t np = 0, nq = 0;
   uint64_t vote_off = 0, vote_cnt = 0;        // certificate votes in the thread arena
+  // Header::digest preimage: author || round_le || (digest || worker_le)* || parent*
+  // (messages.rs:70-84) -- the canonical map/set wire order is already sorted
+  uint64_t pre_len() const { return 40 + 36 * np + 32 * nq; }
+  void write_pre(uint8_t* o) const {
+    std::memcpy(o, author_pk.bytes.data(), 32);
+    std::memcpy(o + 32, &round, 8);
+    std::memcpy(o + 40, pay, 36 * np);
+    std::memcpy(o + 40 + 36 * np, par, 32 * nq);
+  }
 };
 
 struct Arena {
-  std::vector<uint8_t> pre;       // header preimages
   std::vector<uint32_t> vkey;     // certificate vote key indices
   std::vector<const uint8_t*> vsig;  // certificate vote signatures (64 B each, in the wire buffer)
+};
+
+// Grow-only page-locked buffer (nt_host_alloc): the host entry points DMA
+// straight from it instead of staging a copy.
+struct PinnedBuf {
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+  PinnedBuf() = default;
+  PinnedBuf(const PinnedBuf&) = delete;
+  PinnedBuf& operator=(const PinnedBuf&) = delete;
+  ~PinnedBuf() { nt_host_free(p); }
+  template <class T = uint8_t>
+  T* ensure(size_t bytes) {
+    if (bytes > cap || !p) {
+      nt_host_free(p);
+      p = nullptr;
+      cap = 0;
+      const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 20);
+      p = (uint8_t*)nt_host_alloc(want);
+      if (!p) throw crypto::BackendError("nt_host_alloc: no pinned host memory");
+      cap = want;
+    }
+    return (T*)p;
+  }
 };
 
 }  // namespace
@@ -78,9 +145,9 @@ struct Arena {
 struct IngestWorkspace {
   std::vector<Rec> recs;
   std::vector<Arena> arenas;
-  std::vector<uint8_t> need, pre, dig, gsig, gpk;
+  std::vector<uint8_t> need, dig, gpk;
   std::vector<uint64_t> dig_at, poff, plen;
-  std::vector<uint32_t> gkey;
+  PinnedBuf pre, gkey, gsig;  // digest preimages; dense group keys and signatures
   std::vector<DagError> res;
 };
 
@@ -117,32 +184,31 @@ struct Fast {
     if (ok && c > (n - pos) / min_elem) ok = false;
     return ok ? c : 0;
   }
-  // PublicKey string -> committee index (kNoKey if valid but unknown); raw key out
-  uint32_t key(PublicKey& raw) {
+  // PublicKey string -> committee index (kNoKey if valid but unknown); raw key
+  // out unless `raw` is null (vote keys: only the index is used)
+  uint32_t key(PublicKey* raw) {
     const uint64_t len = count(1);
     const uint8_t* s = take(len);
     if (!ok) return kNoKey;
-    auto it = ki.by_b64.find(std::string_view((const char*)s, (size_t)len));
-    if (it != ki.by_b64.end()) {
-      raw = ki.keys[it->second];
-      return it->second;
+    const uint32_t k = ki.find_b64(s, (size_t)len);
+    if (k != KeyIndex::kEmpty) {
+      if (raw) *raw = ki.keys[k];
+      return k;
     }
+    PublicKey tmp;
+    if (!raw) raw = &tmp;
     // not a canonical committee encoding: full serde String + base64 decode
-    if (!decode_public_key(s, (size_t)len, raw)) {
+    if (!decode_public_key(s, (size_t)len, *raw)) {
       ok = false;
       return kNoKey;
     }
-    return ki.of_bytes(raw);
+    return ki.of_bytes(*raw);
   }
   // header fields into rec + preimage into the arena; canonical order checked
-  void header(Rec& r, Arena& a) {
-    r.author = key(r.author_pk);
+  void header(Rec& r) {
+    r.author = key(&r.author_pk);
     r.round = u64();
     if (!ok) return;
-    const size_t p0 = a.pre.size();
-    a.pre.insert(a.pre.end(), r.author_pk.bytes.begin(), r.author_pk.bytes.end());
-    const uint8_t* rb = p + pos - 8;
-    a.pre.insert(a.pre.end(), rb, rb + 8);
     const uint64_t np = count(36);
     const uint8_t* pay = take(36 * np);
     if (!ok) return;
@@ -155,20 +221,20 @@ struct Fast {
         if (!std::binary_search(ws.begin(), ws.end(), w)) r.workers_ok = 0;
       }
     }
-    a.pre.insert(a.pre.end(), pay, pay + 36 * np);
     const uint64_t nq = count(32);
     const uint8_t* par = take(32 * nq);
     if (!ok) return;
     for (uint64_t i = 1; i < nq; ++i)
       if (std::memcmp(par + 32 * (i - 1), par + 32 * i, 32) >= 0) r.status = kRecGeneral;
-    a.pre.insert(a.pre.end(), par, par + 32 * nq);
     const uint8_t* id = take(32);
     const uint8_t* sg = take(64);
     if (!ok) return;
     std::memcpy(r.id.data(), id, 32);
     std::memcpy(r.sig.data(), sg, 64);
-    r.pre_off = p0;
-    r.pre_len = a.pre.size() - p0;
+    r.pay = pay;
+    r.np = np;
+    r.par = par;
+    r.nq = nq;
   }
   void message(Rec& r, Arena& a) {
     const uint32_t tag = u32();
@@ -178,24 +244,23 @@ struct Fast {
     }
     r.kind = (uint8_t)tag;
     if (tag == 0) {
-      header(r, a);
+      header(r);
     } else if (tag == 1) {
       const uint8_t* id = take(32);
       r.round = u64();
-      r.origin = key(r.origin_pk);
-      r.author = key(r.author_pk);
+      r.origin = key(&r.origin_pk);
+      r.author = key(&r.author_pk);
       const uint8_t* sg = take(64);
       if (!ok) return;
       std::memcpy(r.id.data(), id, 32);
       std::memcpy(r.sig.data(), sg, 64);
     } else if (tag == 2) {
-      header(r, a);
+      header(r);
       const uint64_t nv = count(8 + 64);
       r.vote_off = a.vkey.size();
       r.vote_cnt = nv;
       for (uint64_t i = 0; ok && i < nv; ++i) {
-        PublicKey raw;
-        const uint32_t k = key(raw);
+        const uint32_t k = key(nullptr);
         const uint8_t* sg = take(64);
         if (!ok) return;
         a.vkey.push_back(k);
@@ -204,8 +269,7 @@ struct Fast {
     } else {
       const uint64_t nd = count(32);
       take(32 * nd);
-      PublicKey raw;
-      key(raw);
+      key(nullptr);
     }
   }
 };
@@ -251,7 +315,6 @@ std::vector<DagError> Core::ingest_soa(const uint8_t* data, const uint64_t* off,
   std::vector<Arena>& arenas = W.arenas;
   arenas.resize(T);
   for (auto& a : arenas) {
-    a.pre.clear();
     a.vkey.clear();
     a.vsig.clear();
   }
@@ -259,13 +322,12 @@ std::vector<DagError> Core::ingest_soa(const uint8_t* data, const uint64_t* off,
     for (size_t i = lo(t); i < hi(t); ++i) {
       Fast f{data + off[i], (size_t)len[i], 0, true, ki};
       Arena& a = arenas[t];
-      const size_t npre = a.pre.size(), nvote = a.vkey.size();
+      const size_t nvote = a.vkey.size();
       f.message(recs[i], a);
       if (!f.ok) {
         // drop whatever the failed message appended: vkey[k] and vsig[k] must
         // stay the same vote for every later certificate of this thread
         recs[i].status = kRecBad;
-        a.pre.resize(npre);
         a.vkey.resize(nvote);
         a.vsig.resize(nvote);
       }
@@ -298,36 +360,17 @@ std::vector<DagError> Core::ingest_soa(const uint8_t* data, const uint64_t* off,
       for (size_t k = 0; k < gidx.size(); ++k) res[gidx[k]] = r[k];
     }
   }
-  // ---- phase B: round filters + digest preimages, per thread, then concatenated
+  // ---- phase B: round filters, then every digest preimage written once,
+  // straight into the pinned launch buffer (sizes first, then the copies)
   enum Need : uint8_t { kNone, kHeader, kVote, kCert };
   std::vector<uint8_t>& need = W.need;
   need.assign(n, kNone);
   std::vector<uint64_t>& dig_at = W.dig_at;  // thread-local digest index, made global below
   dig_at.assign(n, 0);
   static const std::array<uint8_t, 32> zero{};
-  struct PreBuf {
-    std::vector<uint8_t> bytes;
-    std::vector<uint64_t> off, len;
-  };
-  std::vector<PreBuf> pb(T);
+  std::vector<uint64_t> pre_base(T + 1, 0), dig_base(T + 1, 0);
   parallel_for(T, [&](int t) {
-    PreBuf& b = pb[t];
-    const Arena& a = arenas[t];
-    size_t bytes = 0;
-    for (size_t i = lo(t); i < hi(t); ++i) bytes += recs[i].pre_len + 72;
-    b.bytes.reserve(bytes);
-    auto add = [&](const uint8_t* q, size_t k) {
-      b.off.push_back(b.bytes.size());
-      b.len.push_back(k);
-      b.bytes.insert(b.bytes.end(), q, q + k);
-    };
-    auto add_short = [&](const std::array<uint8_t, 32>& id, uint64_t round, const PublicKey& pk) {
-      uint8_t v[72];  // id || round_le || key (messages.rs:145-153, 226-234)
-      std::memcpy(v, id.data(), 32);
-      std::memcpy(v + 32, &round, 8);
-      std::memcpy(v + 40, pk.bytes.data(), 32);
-      add(v, 72);
-    };
+    uint64_t bytes = 0, nd = 0;
     for (size_t i = lo(t); i < hi(t); ++i) {
       const Rec& r = recs[i];
       if (r.status == kRecBad) { res[i] = DagError::SerializationError; continue; }
@@ -336,8 +379,8 @@ std::vector<DagError> Core::ingest_soa(const uint8_t* data, const uint64_t* off,
         case 0:
           if (r.round < gc_round) { res[i] = DagError::TooOld; break; }
           need[i] = kHeader;
-          dig_at[i] = b.off.size();
-          add(a.pre.data() + r.pre_off, r.pre_len);
+          bytes += r.pre_len();
+          nd += 1;
           break;
         case 1:
           if (r.round < current_header.round) { res[i] = DagError::TooOld; break; }
@@ -347,83 +390,90 @@ std::vector<DagError> Core::ingest_soa(const uint8_t* data, const uint64_t* off,
             break;
           }
           need[i] = kVote;
-          dig_at[i] = b.off.size();
-          add_short(r.id, r.round, r.origin_pk);
+          bytes += 72;
+          nd += 1;
           break;
         case 2:
           if (r.round < gc_round) { res[i] = DagError::TooOld; break; }
           if (r.id == zero && r.round == 0 && r.author != kNoKey) break;  // genesis
           need[i] = kCert;
-          dig_at[i] = b.off.size();
-          add(a.pre.data() + r.pre_off, r.pre_len);
-          add_short(r.id, r.round, r.author_pk);
+          bytes += r.pre_len() + 72;
+          nd += 2;
           break;
         default: res[i] = DagError::UnexpectedMessage; break;
       }
     }
+    pre_base[t + 1] = bytes;
+    dig_base[t + 1] = nd;
   });
-  std::vector<uint64_t> pre_base(T + 1, 0), dig_base(T + 1, 0);
   for (int t = 0; t < T; ++t) {
-    pre_base[t + 1] = pre_base[t] + pb[t].bytes.size();
-    dig_base[t + 1] = dig_base[t] + pb[t].off.size();
+    pre_base[t + 1] += pre_base[t];
+    dig_base[t + 1] += dig_base[t];
   }
   const size_t nd = dig_base[T];
-  std::vector<uint8_t>& pre = W.pre;
-  pre.resize(std::max<uint64_t>(pre_base[T], 1));
+  uint8_t* pre = W.pre.ensure(std::max<uint64_t>(pre_base[T], 1));
   std::vector<uint64_t>& poff = W.poff;
   std::vector<uint64_t>& plen = W.plen;
   poff.resize(std::max<size_t>(nd, 1));
   plen.resize(std::max<size_t>(nd, 1));
   parallel_for(T, [&](int t) {
-    std::memcpy(pre.data() + pre_base[t], pb[t].bytes.data(), pb[t].bytes.size());
-    for (size_t k = 0; k < pb[t].off.size(); ++k) {
-      poff[dig_base[t] + k] = pre_base[t] + pb[t].off[k];
-      plen[dig_base[t] + k] = pb[t].len[k];
+    uint64_t o = pre_base[t], d = dig_base[t];
+    auto add_short = [&](const std::array<uint8_t, 32>& id, uint64_t round, const PublicKey& pk) {
+      // id || round_le || key (messages.rs:145-153, 226-234)
+      std::memcpy(pre + o, id.data(), 32);
+      std::memcpy(pre + o + 32, &round, 8);
+      std::memcpy(pre + o + 40, pk.bytes.data(), 32);
+      poff[d] = o;
+      plen[d] = 72;
+      o += 72;
+      ++d;
+    };
+    for (size_t i = lo(t); i < hi(t); ++i) {
+      const Rec& r = recs[i];
+      if (need[i] == kNone) continue;
+      dig_at[i] = d;
+      if (need[i] == kVote) {
+        add_short(r.id, r.round, r.origin_pk);
+        continue;
+      }
+      r.write_pre(pre + o);
+      poff[d] = o;
+      plen[d] = r.pre_len();
+      o += r.pre_len();
+      ++d;
+      if (need[i] == kCert) add_short(r.id, r.round, r.author_pk);
     }
-    for (size_t i = lo(t); i < hi(t); ++i) dig_at[i] += dig_base[t];
-    std::vector<uint8_t>().swap(pb[t].bytes);
   });
   nt_ctx* ctx = crypto::Backend::global().ctx();
   st.prep += since(tp);
   tp = std::chrono::steady_clock::now();
   std::vector<uint8_t>& dig = W.dig;
   dig.resize(32 * std::max<size_t>(nd, 1));
-  if (nd) check(nt_sha512_trunc32(ctx, pre.data(), poff.data(), plen.data(), nd, dig.data()), "nt_sha512_trunc32");
+  if (nd) check(nt_sha512_trunc32(ctx, pre, poff.data(), plen.data(), nd, dig.data()), "nt_sha512_trunc32");
   st.digest = since(tp);
   tp = std::chrono::steady_clock::now();
 
-  // ---- phase C: prechecks in the reference order, per thread; the vote arrays
-  // of all arenas are concatenated once and certificate groups point into them
-  std::vector<uint64_t> vbase(T + 1, 0);
-  for (int t = 0; t < T; ++t) vbase[t + 1] = vbase[t] + arenas[t].vkey.size();
-  const uint64_t nv = vbase[T];
-  std::vector<uint32_t>& gkey = W.gkey;
-  std::vector<uint8_t>& gsig = W.gsig;
-  std::vector<uint8_t>& gpk = W.gpk;
-  gkey.resize(std::max<uint64_t>(nv, 1));
-  gsig.resize(64 * std::max<uint64_t>(nv, 1));
-  gpk.resize(cache ? 0 : 32 * std::max<uint64_t>(nv, 1));
+  // ---- phase C: prechecks in the reference order, per thread; then the votes
+  // of the certificates that passed are packed densely, in group order, into
+  // the pinned key / signature buffers the verify_batch launch reads directly
   struct SigOut {
     std::vector<uint32_t> key;
     std::vector<uint8_t> pk, sig, msg;
     std::vector<size_t> who;                 // message index per strict entry
-    std::vector<uint64_t> first;             // groups: global vote offset
+    std::vector<uint64_t> first;             // groups: thread-local dense vote offset
     std::vector<uint32_t> cnt;
     std::vector<uint8_t> gmsg;
     std::vector<size_t> gwho;
   };
   std::vector<SigOut> so(T);
   const Stake quorum = cm.quorum_threshold();
+  std::vector<uint64_t> vbase(T + 1, 0);
   parallel_for(T, [&](int t) {
     const Arena& a = arenas[t];
-    std::memcpy(gkey.data() + vbase[t], a.vkey.data(), 4 * a.vkey.size());
-    for (size_t k = 0; k < a.vsig.size(); ++k) std::memcpy(&gsig[64 * (vbase[t] + k)], a.vsig[k], 64);
-    if (!cache)
-      for (size_t k = 0; k < a.vkey.size(); ++k)
-        if (a.vkey[k] != kNoKey) std::memcpy(&gpk[32 * (vbase[t] + k)], ki.keys[a.vkey[k]].bytes.data(), 32);
     SigOut& o = so[t];
     std::vector<uint32_t> stamp(ki.keys.size(), 0);
     uint32_t stamp_id = 0;
+    uint64_t dense = 0;
     auto add_sig = [&](size_t i, uint32_t key, const std::array<uint8_t, 64>& sg, const uint8_t* msg) {
       o.who.push_back(i);
       o.key.push_back(key);
@@ -452,14 +502,37 @@ std::vector<DagError> Core::ingest_soa(const uint8_t* data, const uint64_t* off,
           if (e == DagError::Ok && weight < quorum) e = DagError::CertificateRequiresQuorum;
           if (e != DagError::Ok) { res[i] = e; continue; }
           o.gwho.push_back(i);
-          o.first.push_back(vbase[t] + r.vote_off);
+          o.first.push_back(dense);
           o.cnt.push_back((uint32_t)r.vote_cnt);
           o.gmsg.insert(o.gmsg.end(), d + 32, d + 64);
+          dense += r.vote_cnt;
         }
         add_sig(i, r.author, r.sig, r.id.data());
       } else if (need[i] == kVote) {
         if (r.author == kNoKey || ki.stake[r.author] == 0) { res[i] = DagError::UnknownAuthority; continue; }
         add_sig(i, r.author, r.sig, d);
+      }
+    }
+    vbase[t + 1] = dense;
+  });
+  for (int t = 0; t < T; ++t) vbase[t + 1] += vbase[t];
+  const uint64_t nv = vbase[T];
+  uint32_t* gkey = W.gkey.ensure<uint32_t>(4 * std::max<uint64_t>(nv, 1));
+  uint8_t* gsig = W.gsig.ensure(64 * std::max<uint64_t>(nv, 1));
+  std::vector<uint8_t>& gpk = W.gpk;
+  gpk.resize(cache ? 0 : 32 * std::max<uint64_t>(nv, 1));
+  parallel_for(T, [&](int t) {
+    const Arena& a = arenas[t];
+    SigOut& o = so[t];
+    for (size_t k = 0; k < o.gwho.size(); ++k) {
+      const Rec& r = recs[o.gwho[k]];
+      const uint64_t dst = vbase[t] + o.first[k];
+      o.first[k] = dst;
+      for (uint64_t v = 0; v < r.vote_cnt; ++v) {
+        const uint32_t key = a.vkey[r.vote_off + v];
+        gkey[dst + v] = key;
+        std::memcpy(gsig + 64 * (dst + v), a.vsig[r.vote_off + v], 64);
+        if (!cache) std::memcpy(&gpk[32 * (dst + v)], ki.keys[key].bytes.data(), 32);
       }
     }
   });
@@ -497,11 +570,11 @@ std::vector<DagError> Core::ingest_soa(const uint8_t* data, const uint64_t* off,
   tp = std::chrono::steady_clock::now();
   if (G) {
     if (cache)
-      check(nt_ed25519_verify_batch_groups_keyset(ctx, cache->handle(), gkey.data(), gsig.data(), all.first.data(),
+      check(nt_ed25519_verify_batch_groups_keyset(ctx, cache->handle(), gkey, gsig, all.first.data(),
                                                   all.cnt.data(), all.gmsg.data(), G, gbm.data(), nullptr),
             "nt_ed25519_verify_batch_groups_keyset");
     else
-      check(nt_ed25519_verify_batch_groups(ctx, gpk.data(), gsig.data(), all.first.data(), all.cnt.data(),
+      check(nt_ed25519_verify_batch_groups(ctx, gpk.data(), gsig, all.first.data(), all.cnt.data(),
                                            all.gmsg.data(), G, gbm.data(), nullptr),
             "nt_ed25519_verify_batch_groups");
   }

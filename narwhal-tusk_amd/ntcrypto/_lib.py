@@ -27,7 +27,7 @@ EXPORTED = [
     "nt_ed25519_sign_batch", "nt_ed25519_keypair_batch", "nt_dev_sha512_trunc32",
     "nt_dev_ed25519_verify", "nt_dev_group_and", "nt_dev_ed25519_sign", "nt_keyset_create",
     "nt_keyset_free", "nt_keyset_flags", "nt_ed25519_verify_keyset", "nt_ed25519_verify_batch_groups_keyset",
-    "nt_dev_ed25519_verify_keyset",
+    "nt_dev_ed25519_verify_keyset", "nt_host_alloc", "nt_host_free",
 ]
 
 
@@ -52,6 +52,10 @@ def load_library(path=None):
     lib.nt_init_devices.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     lib.nt_free.argtypes = [_vp]
     lib.nt_free.restype = None
+    lib.nt_host_alloc.argtypes = [ctypes.c_uint64]
+    lib.nt_host_alloc.restype = _vp
+    lib.nt_host_free.argtypes = [_vp]
+    lib.nt_host_free.restype = None
     lib.nt_num_devices.argtypes = [_vp]
     lib.nt_strerror.restype = ctypes.c_char_p
     lib.nt_version.restype = ctypes.c_char_p
