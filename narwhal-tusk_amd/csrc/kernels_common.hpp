@@ -22,6 +22,9 @@ constexpr int kAQuads = 10;           // uint4 per cached entry (40 words)
 struct WideComb {
   const uint32_t* base;
   NT_D NT_INLINE void load(uint32_t pos, uint32_t idx, ge_niels& q) const {
+#ifdef NT_EXPERIMENT_CACHED_COMB
+    idx &= 7;  // timing experiment only (wrong results): every lookup hits in cache
+#endif
     const uint4* e = (const uint4*)(base + ((size_t)pos * kWEntries + idx) * kWStride);
     uint32_t w[32];
 #pragma unroll
