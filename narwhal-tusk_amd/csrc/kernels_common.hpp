@@ -41,7 +41,10 @@ struct WideComb {
   }
 };
 
-constexpr size_t kWWordsPerKey = (size_t)kWPos * kWEntries * kWStride;
+#ifndef NT_EXPERIMENT_KEY_STRIDE
+#define NT_EXPERIMENT_KEY_STRIDE 1  // timing experiment: spread keys' combs over N x the address space
+#endif
+constexpr size_t kWWordsPerKey = (size_t)kWPos * kWEntries * kWStride * NT_EXPERIMENT_KEY_STRIDE;
 
 // j*(-A) entries in the global workspace, layout [slot][entry][quad][lane] of
 // uint4: a lane's 16-byte accesses are adjacent to its neighbours'.
