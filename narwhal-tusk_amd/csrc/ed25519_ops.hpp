@@ -42,37 +42,67 @@ NT_HD NT_INLINE void ld8(uint32_t w[8], const uint32_t* p) {
 }
 
 // ---------------------------------------------------------------------------
-// Wide combs: for a fixed point P, entry (i, j) = j * 2^(16 i) * P as affine
-// niels, i in [0, 16), j in [0, 2^15].  [x]P is then 16 mixed additions and no
-// doublings (signed radix-2^16 digits of x).  67 MB per point: sized for the
-// MI355X's 288 GB of HBM -- one comb of B per device, one per committee key.
+// Wide combs: for a fixed point P and digit width W, entry (i, j) =
+// j * 2^(W i) * P as affine niels, i in [0, pos), j in [0, 2^(W-1)].  [x]P is
+// then `pos` mixed additions and no doublings (signed radix-2^W digits of x).
+//   W = 20: 13 additions, 872 MB per point  (the base point; committee keys
+//           while they fit: 100 keys = 87 GB of the MI355X's 288 GB of HBM3E)
+//   W = 16: 16 additions,  67 MB per point  (committee keys otherwise)
+// Layout [pos][entry][kWStride words]; a table access type carries its W as
+// `kBits` (WideComb<W> on the device, HostWComb<W> in the host harness).
 // ---------------------------------------------------------------------------
-constexpr int kWPos = 16;
-constexpr int kWEntries = 32769;   // |digit| in 0..2^15
-constexpr int kWStride = 32;       // words per entry (30 used)
-constexpr int kWChunk = 64;        // consecutive entries built by one thread
-constexpr int kWChunks = 512;      // chunks per position: entries 1..32768
+constexpr int kWStride = 32;  // words per entry (30 used)
+constexpr int kWChunk = 64;   // consecutive entries built by one thread
+#ifndef NT_BCOMB_BITS
+#define NT_BCOMB_BITS 20
+#endif
+constexpr int kBCombBits = NT_BCOMB_BITS;  // comb of the base point B (one per device)
+static_assert(kBCombBits == kKeyCombWide || kBCombBits == kKeyCombNarrow, "B comb width must be a built width");
+
+template <int W>
+struct CombGeom {
+  static_assert(W >= 12 && W <= 22, "comb digit width");
+  static constexpr int kPos = (254 + W - 1) / W;          // signed digits of a 253-bit scalar
+  static constexpr int kEntries = (1 << (W - 1)) + 1;     // |digit| in 0..2^(W-1)
+  static constexpr int kChunks = (1 << (W - 1)) / kWChunk;  // chunks per position: entries 1..2^(W-1)
+  static constexpr size_t kWordsPerPoint = (size_t)kPos * kEntries * kWStride;
+  // the top digit of any x < 2^253 (every scalar of a passing check) never goes
+  // negative, so no carry is lost: the bits above (kPos-1) W plus a carry are <= 2^(W-1)
+  static_assert(253 - (kPos - 1) * W <= W - 1, "top comb digit must absorb the carry");
+};
+
+// Next signed radix-2^W digit of the scalar held in d (d >>= W), in
+// [-2^(W-1)+1, 2^(W-1)] for ANY 256-bit input (an unchecked s >= L only yields
+// a wrong point, never an out-of-range table index; its verdict is reject).
+template <int W>
+NT_HD NT_INLINE int32_t wcomb_digit(uint32_t d[8], uint32_t& carry) {
+  const uint32_t raw = (d[0] & ((1u << W) - 1u)) + carry;
+  carry = raw > (1u << (W - 1)) ? 1u : 0u;
+#pragma unroll
+  for (int m = 0; m < 7; ++m) d[m] = (d[m] >> W) | (d[m + 1] << (32 - W));
+  d[7] >>= W;
+  return (int32_t)raw - (int32_t)(carry << W);
+}
 
 // acc += [x]P with P's wide comb.  The table load of digit i+1 is issued right
 // after the multiplies that consume entry i, so its latency (a random 128-B
 // line) overlaps the rest of the addition.
 template <class WComb>
 NT_HD NT_INLINE void wcomb_acc(ge_p3& acc, const uint32_t x[8], const WComb& wc) {
-  uint32_t d[8];
-  sc_recode_w16(d, x);
-  int32_t dg = (int32_t)(int16_t)(uint16_t)(d[0] & 0xffffu);
+  constexpr int W = WComb::kBits, P = CombGeom<W>::kPos;
+  uint32_t d[8], carry = 0;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) d[m] = x[m];
+  int32_t dg = wcomb_digit<W>(d, carry);
   ge_niels ne;
   wc.load(0, (uint32_t)(dg < 0 ? -dg : dg), ne);
 #pragma unroll 1
-  for (int pos = 0; pos < kWPos; ++pos) {
-#pragma unroll
-    for (int m = 0; m < 7; ++m) d[m] = (d[m] >> 16) | (d[m + 1] << 16);
-    d[7] >>= 16;
+  for (int pos = 0; pos < P; ++pos) {
     ge_niels_cneg(ne, dg < 0);
     fe PP, MM, TT;
     ge_add_niels_1(PP, MM, TT, acc, ne);
-    const int32_t dn = (int32_t)(int16_t)(uint16_t)(d[0] & 0xffffu);
-    const int nxt = pos + 1 < kWPos ? pos + 1 : pos;  // last round reloads a valid entry
+    const int32_t dn = wcomb_digit<W>(d, carry);  // past the last position: a harmless in-range digit
+    const int nxt = pos + 1 < P ? pos + 1 : pos;   // last round reloads a valid entry
     wc.load(nxt, (uint32_t)(dn < 0 ? -dn : dn), ne);
     dg = dn;
     ge_cp t;
@@ -81,12 +111,13 @@ NT_HD NT_INLINE void wcomb_acc(ge_p3& acc, const uint32_t x[8], const WComb& wc)
   }
 }
 
-// Wide-comb construction, step 1 (one thread per point): P_i = 2^(16 i) P,
+// Wide-comb construction, step 1 (one thread per point): P_i = 2^(W i) P,
 // stored as p3 limbs [i][X,Y,Z,T][10].
+template <int W>
 NT_HD NT_INLINE void wcomb_bases(uint32_t* out, const ge_p3& P0) {
   ge_p3 P = P0;
 #pragma unroll 1
-  for (int i = 0; i < kWPos; ++i) {
+  for (int i = 0; i < CombGeom<W>::kPos; ++i) {
     uint32_t* o = out + 40 * i;
 #pragma unroll
     for (int l = 0; l < 10; ++l) {
@@ -95,7 +126,7 @@ NT_HD NT_INLINE void wcomb_bases(uint32_t* out, const ge_p3& P0) {
     ge_p2 q;
     ge_p3_to_p2(q, P);
 #pragma unroll 1
-    for (int r = 0; r < 15; ++r) ge_dbl_p2(q, q);
+    for (int r = 0; r < W - 1; ++r) ge_dbl_p2(q, q);
     ge_cp t;
     ge_dbl(t, q);
     ge_cp_to_p3(P, t);
@@ -106,6 +137,7 @@ NT_HD NT_INLINE void wcomb_bases(uint32_t* out, const ge_p3& P0) {
 // with j0 = 1 + 64 c, written to dst (entry j0 first, kWStride words each);
 // chunk 0 also writes entry 0 (identity) at dst - kWStride.  One inversion per
 // chunk (Montgomery's trick); tmp holds the 64 prefix products (640 words).
+template <int W>
 NT_HD NT_INLINE void wcomb_fill(uint32_t* dst, uint32_t* tmp, const uint32_t* base, uint32_t c) {
   ge_p3 P;
 #pragma unroll
@@ -114,13 +146,13 @@ NT_HD NT_INLINE void wcomb_fill(uint32_t* dst, uint32_t* tmp, const uint32_t* ba
   }
   ge_cached Pc;
   ge_p3_to_cached(Pc, P);
-  // Q = j0 * P by double-and-add over the 16 bits of j0
+  // Q = j0 * P by double-and-add over the W bits of j0
   const uint32_t j0 = 1u + (uint32_t)kWChunk * c;
   ge_p3 Q;
   ge_p3_0(Q);
   ge_cp t;
 #pragma unroll 1
-  for (int bit = 15; bit >= 0; --bit) {
+  for (int bit = W - 1; bit >= 0; --bit) {
     ge_p2 q2;
     ge_p3_to_p2(q2, Q);
     ge_dbl(t, q2);

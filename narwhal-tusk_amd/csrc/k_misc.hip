@@ -148,9 +148,10 @@ __global__ __launch_bounds__(128) void k_sha512_pipe(const uint8_t* __restrict__
 // --------------------------------------------------------------------------
 // Wide-comb construction
 // --------------------------------------------------------------------------
-// One thread per point: decode (or take B), optionally negate, write the 16
-// bases 2^(16 i) P.  meta[key] gets the kKey* bits.  Keys that do not decode get
+// One thread per point: decode (or take B), optionally negate, write the
+// kPos bases 2^(W i) P.  meta[key] gets the kKey* bits.  Keys that do not decode get
 // identity bases (every entry the identity; such keys always reject via meta).
+template <int W>
 __global__ void k_wcomb_bases(const uint32_t* __restrict__ enc, uint32_t nkeys, int negate,
                               uint32_t* __restrict__ bases, uint32_t* __restrict__ meta) {
   const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
@@ -168,20 +169,22 @@ __global__ void k_wcomb_bases(const uint32_t* __restrict__ enc, uint32_t nkeys, 
     fe_neg(P.T, P.T);
     fe_carry(P.T);
   }
-  wcomb_bases(bases + (size_t)key * kWPos * 40, P);
+  wcomb_bases<W>(bases + (size_t)key * CombGeom<W>::kPos * 40, P);
 }
 
 // One thread per (key, position, chunk of 64 entries).
+template <int W>
 __global__ void k_wcomb_fill(const uint32_t* __restrict__ bases, uint32_t nkeys, uint32_t* __restrict__ comb,
                              uint32_t* __restrict__ tmp) {
+  using G = CombGeom<W>;
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t per_key = (uint64_t)kWPos * kWChunks;
+  const uint64_t per_key = (uint64_t)G::kPos * G::kChunks;
   if (t >= per_key * nkeys) return;
   const uint32_t key = (uint32_t)(t / per_key);
-  const uint32_t pos = (uint32_t)((t % per_key) / kWChunks);
-  const uint32_t c = (uint32_t)(t % kWChunks);
-  uint32_t* dst = comb + key * kWWordsPerKey + ((size_t)pos * kWEntries + 1 + (size_t)kWChunk * c) * kWStride;
-  wcomb_fill(dst, tmp + t * (kWChunk * 10), bases + ((size_t)key * kWPos + pos) * 40, c);
+  const uint32_t pos = (uint32_t)((t % per_key) / G::kChunks);
+  const uint32_t c = (uint32_t)(t % G::kChunks);
+  uint32_t* dst = comb + key * G::kWordsPerPoint + ((size_t)pos * G::kEntries + 1 + (size_t)kWChunk * c) * kWStride;
+  wcomb_fill<W>(dst, tmp + t * (kWChunk * 10), bases + ((size_t)key * G::kPos + pos) * 40, c);
 }
 
 // --------------------------------------------------------------------------
@@ -235,7 +238,7 @@ __global__ __launch_bounds__(kBlock) void k_ed25519_sign(const uint32_t* __restr
                                                         const uint32_t* __restrict__ combB,
                                                         uint32_t* __restrict__ out_pk,
                                                         uint32_t* __restrict__ out_sig) {
-  const WideComb wb{combB};
+  const BComb wb{combB};
   for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < n; base += (uint64_t)gridDim.x * kBlock) {
     const uint64_t gi = base + threadIdx.x;
     const uint32_t active = gi < n;
@@ -330,32 +333,45 @@ hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, const uint64
   return hipGetLastError();
 }
 
-// Builds the wide combs of nkeys points, `batch` keys per fill launch (tmp must
-// hold wcomb_fill_tmp_bytes_per_key() * batch bytes; bases nkeys * wcomb_bases_bytes_per_key()).
-hipError_t launch_wcomb_build(const uint32_t* d_enc, uint32_t nkeys, int negate, uint32_t* d_comb,
-                              uint32_t* d_meta, uint32_t* d_bases, uint32_t* d_tmp, uint32_t batch,
-                              hipStream_t s) {
-  if (nkeys == 0) return hipSuccess;
-  if (batch == 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_wcomb_bases, dim3((nkeys + 63) / 64), dim3(64), 0, s, d_enc, nkeys, negate, d_bases,
+// Builds the W-bit wide combs of nkeys points, `batch` keys per fill launch (tmp
+// must hold wcomb_fill_tmp_bytes_per_key(W) * batch bytes; bases nkeys *
+// wcomb_bases_bytes_per_key(W)).
+template <int W>
+static hipError_t wcomb_build(const uint32_t* d_enc, uint32_t nkeys, int negate, uint32_t* d_comb,
+                              uint32_t* d_meta, uint32_t* d_bases, uint32_t* d_tmp, uint32_t batch, hipStream_t s) {
+  using G = CombGeom<W>;
+  hipLaunchKernelGGL(k_wcomb_bases<W>, dim3((nkeys + 63) / 64), dim3(64), 0, s, d_enc, nkeys, negate, d_bases,
                      d_meta);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   for (uint32_t k0 = 0; k0 < nkeys; k0 += batch) {
     const uint32_t nk = nkeys - k0 < batch ? nkeys - k0 : batch;
-    const uint64_t threads = (uint64_t)nk * kWPos * kWChunks;
-    hipLaunchKernelGGL(k_wcomb_fill, dim3((uint32_t)((threads + 63) / 64)), dim3(64), 0, s,
-                       d_bases + (size_t)k0 * kWPos * 40, nk, d_comb + (size_t)k0 * kWWordsPerKey, d_tmp);
+    const uint64_t threads = (uint64_t)nk * G::kPos * G::kChunks;
+    hipLaunchKernelGGL(k_wcomb_fill<W>, dim3((uint32_t)((threads + 63) / 64)), dim3(64), 0, s,
+                       d_bases + (size_t)k0 * G::kPos * 40, nk, d_comb + (size_t)k0 * G::kWordsPerPoint, d_tmp);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
 }
 
+hipError_t launch_wcomb_build(int bits, const uint32_t* d_enc, uint32_t nkeys, int negate, uint32_t* d_comb,
+                              uint32_t* d_meta, uint32_t* d_bases, uint32_t* d_tmp, uint32_t batch,
+                              hipStream_t s) {
+  if (nkeys == 0) return hipSuccess;
+  if (batch == 0) return hipErrorInvalidValue;
+  switch (bits) {
+    case kKeyCombWide: return wcomb_build<kKeyCombWide>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
+    case kKeyCombNarrow:
+      return wcomb_build<kKeyCombNarrow>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 // signatures per key-cache launch (a multiple of 64: verdict words stay aligned)
 constexpr uint64_t kKsMaxPerLaunch = 8ull << 20;
 
-hipError_t launch_verify_keyset(int mode, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
+hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                                 const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                                 const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
                                 const uint32_t* d_combB, void* d_stash, uint64_t* d_out_words, hipStream_t s) {
@@ -363,21 +379,44 @@ hipError_t launch_verify_keyset(int mode, const uint32_t* d_key_idx, const uint8
   for (uint64_t lo = 0; lo < n; lo += kKsMaxPerLaunch) {
     const uint64_t m = n - lo < kKsMaxPerLaunch ? n - lo : kKsMaxPerLaunch;
     const uint64_t blocks = keyset_blocks(m);
-    const hipError_t e =
-        mode == kStrict
-            ? launch_keyset_m<kStrict>(blocks, d_key_idx + lo, d_sig + 64 * lo, d_msg, d_off + lo, d_len + lo, m,
-                                       d_meta, d_enc, d_combA, nkeys, d_combB, d_stash, d_out_words + lo / 64, s)
-            : launch_keyset_m<kCofactorless>(blocks, d_key_idx + lo, d_sig + 64 * lo, d_msg, d_off + lo, d_len + lo,
-                                             m, d_meta, d_enc, d_combA, nkeys, d_combB, d_stash,
-                                             d_out_words + lo / 64, s);
+#define NT_KS_ARGS                                                                                           \
+  blocks, d_key_idx + lo, d_sig + 64 * lo, d_msg, d_off + lo, d_len + lo, m, d_meta, d_enc, d_combA, nkeys, \
+      d_combB, d_stash, d_out_words + lo / 64, s
+    hipError_t e;
+    if (key_bits == kKeyCombWide)
+      e = mode == kStrict ? launch_keyset_m<kStrict, kKeyCombWide>(NT_KS_ARGS)
+                          : launch_keyset_m<kCofactorless, kKeyCombWide>(NT_KS_ARGS);
+    else if (key_bits == kKeyCombNarrow)
+      e = mode == kStrict ? launch_keyset_m<kStrict, kKeyCombNarrow>(NT_KS_ARGS)
+                          : launch_keyset_m<kCofactorless, kKeyCombNarrow>(NT_KS_ARGS);
+    else
+      e = hipErrorInvalidValue;
+#undef NT_KS_ARGS
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
 }
 
-size_t wcomb_bytes_per_key() { return kWWordsPerKey * 4; }
-size_t wcomb_bases_bytes_per_key() { return (size_t)kWPos * 40 * 4; }
-size_t wcomb_fill_tmp_bytes_per_key() { return (size_t)kWPos * kWChunks * kWChunk * 10 * 4; }
+template <int W>
+static size_t comb_size(int what) {
+  using G = CombGeom<W>;
+  switch (what) {
+    case 0: return G::kWordsPerPoint * 4;
+    case 1: return (size_t)G::kPos * 40 * 4;
+    case 2: return (size_t)G::kPos * G::kChunks * kWChunk * 10 * 4;
+    default: return (size_t)std::max<uint64_t>(1, (128u << 10) / ((uint64_t)G::kPos * G::kChunks));
+  }
+}
+static size_t comb_size(int bits, int what) {
+  return bits == kKeyCombWide ? comb_size<kKeyCombWide>(what)
+         : bits == kKeyCombNarrow ? comb_size<kKeyCombNarrow>(what) : 0;
+}
+size_t wcomb_bytes_per_key(int bits) { return comb_size(bits, 0); }
+size_t wcomb_bases_bytes_per_key(int bits) { return comb_size(bits, 1); }
+size_t wcomb_fill_tmp_bytes_per_key(int bits) { return comb_size(bits, 2); }
+// keys per fill launch: >= 128k threads per launch (16 keys at W = 16, 2 at W = 20)
+uint32_t wcomb_fill_batch(int bits) { return (uint32_t)comb_size(bits, 3); }
+int bcomb_bits() { return kBCombBits; }
 // verify grid: one 512-signature block per workspace slot, at most ws_slots
 uint64_t verify_grid(uint64_t n, uint32_t ws_slots) {
   const uint64_t blocks = (n + 2 * kBlock - 1) / (2 * kBlock);  // two signatures per lane

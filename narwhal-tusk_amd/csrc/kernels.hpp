@@ -4,6 +4,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "nt_common.hpp"
+
 namespace nt {
 
 hipError_t launch_sha512_trunc32(const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
@@ -20,10 +22,11 @@ hipError_t launch_group_msgs(const uint64_t* d_first, const uint32_t* d_cnt, uin
 hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, const uint64_t* d_off,
                        const uint64_t* d_len, uint64_t n, const uint32_t* d_combB, uint8_t* d_pk,
                        uint8_t* d_sig, uint32_t max_blocks, hipStream_t s);
-hipError_t launch_wcomb_build(const uint32_t* d_enc, uint32_t nkeys, int negate, uint32_t* d_comb,
+// wide combs with `bits`-bit digits (kKeyCombWide or kKeyCombNarrow)
+hipError_t launch_wcomb_build(int bits, const uint32_t* d_enc, uint32_t nkeys, int negate, uint32_t* d_comb,
                               uint32_t* d_meta, uint32_t* d_bases, uint32_t* d_tmp, uint32_t batch,
                               hipStream_t s);
-hipError_t launch_verify_keyset(int mode, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
+hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                                 const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                                 const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
                                 const uint32_t* d_combB, void* d_stash, uint64_t* d_out_words, hipStream_t s);
@@ -34,9 +37,11 @@ uint64_t verify_grid(uint64_t n, uint32_t ws_slots);  // blocks of a launch_veri
 uint64_t verify_round_sigs(uint32_t cus);
 uint64_t keyset_blocks(uint64_t n);
 size_t keyset_stash_bytes(uint64_t n);
-size_t wcomb_bytes_per_key();
-size_t wcomb_bases_bytes_per_key();
-size_t wcomb_fill_tmp_bytes_per_key();
+size_t wcomb_bytes_per_key(int bits);
+size_t wcomb_bases_bytes_per_key(int bits);
+size_t wcomb_fill_tmp_bytes_per_key(int bits);
+uint32_t wcomb_fill_batch(int bits);  // keys per k_wcomb_fill launch
+int bcomb_bits();                     // digit width of the base-point comb
 size_t ws_bytes_per_slot();
 int verify_occupancy();  // waves per SIMD of the selected verify kernel variant
 

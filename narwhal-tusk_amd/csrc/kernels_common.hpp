@@ -18,14 +18,17 @@ constexpr int kAQuads = 10;           // uint4 per cached entry (40 words)
 // --------------------------------------------------------------------------
 // Table accessors
 // --------------------------------------------------------------------------
-// Wide comb of one point, layout [pos][entry][32 words]; 8 x 16-byte loads.
+// Wide comb of one point with digit width W, layout [pos][entry][32 words];
+// 8 x 16-byte loads.
+template <int W>
 struct WideComb {
+  static constexpr int kBits = W;
   const uint32_t* base;
   NT_D NT_INLINE void load(uint32_t pos, uint32_t idx, ge_niels& q) const {
 #ifdef NT_EXPERIMENT_CACHED_COMB
     idx &= 7;  // timing experiment only (wrong results): every lookup hits in cache
 #endif
-    const uint4* e = (const uint4*)(base + ((size_t)pos * kWEntries + idx) * kWStride);
+    const uint4* e = (const uint4*)(base + ((size_t)pos * CombGeom<W>::kEntries + idx) * kWStride);
     uint32_t w[32];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -40,11 +43,7 @@ struct WideComb {
     }
   }
 };
-
-#ifndef NT_EXPERIMENT_KEY_STRIDE
-#define NT_EXPERIMENT_KEY_STRIDE 1  // timing experiment: spread keys' combs over N x the address space
-#endif
-constexpr size_t kWWordsPerKey = (size_t)kWPos * kWEntries * kWStride * NT_EXPERIMENT_KEY_STRIDE;
+using BComb = WideComb<kBCombBits>;
 
 // j*(-A) entries in the global workspace, layout [slot][entry][quad][lane] of
 // uint4: a lane's 16-byte accesses are adjacent to its neighbours'.
@@ -81,7 +80,10 @@ struct WsATab {
 };
 
 // ---- key-cache verification: 4 signatures per lane, one inversion ----------
-constexpr int kKsPerLane = 4;
+#ifndef NT_KS_PER_LANE
+#define NT_KS_PER_LANE 4
+#endif
+constexpr int kKsPerLane = NT_KS_PER_LANE;  // signatures per lane sharing one inversion
 constexpr int kKsQuads = 10;  // X, Y, Z, prefix: 40 words per (signature, lane)
 constexpr size_t kKsStashQuadsPerBlock = (size_t)kKsPerLane * kKsQuads * kBlock;
 
@@ -127,7 +129,7 @@ template <int MODE>
 hipError_t launch_verify_m(uint64_t blocks, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
                            const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_combB,
                            void* d_ws, uint64_t* d_out_words, hipStream_t s);
-template <int MODE>
+template <int MODE, int WA>
 hipError_t launch_keyset_m(uint64_t blocks, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                            const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                            const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,

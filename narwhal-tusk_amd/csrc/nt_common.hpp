@@ -29,4 +29,8 @@ enum VerifyMode : int {
   kCofactorless = 1,  // per-entry rule of dalek verify_batch, SURVEY.md A.3
 };
 
+// Digit widths of the committee-key combs (ed25519_ops.hpp, wide combs)
+constexpr int kKeyCombWide = 20;    // 13 additions per [k]A, 872 MB per key: used when they fit in HBM
+constexpr int kKeyCombNarrow = 16;  // 16 additions, 67 MB per key
+
 }  // namespace nt

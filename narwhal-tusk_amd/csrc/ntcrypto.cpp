@@ -147,8 +147,8 @@ struct Device {
     {
       static const uint32_t kB[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                                      0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
-      if (hipMalloc(&d_combB, nt::wcomb_bytes_per_key()) != hipSuccess) return NT_ENOMEM;
-      NT_CHK0(build_wcombs(kB, 1, 0, d_combB, nullptr));
+      if (hipMalloc(&d_combB, nt::wcomb_bytes_per_key(nt::bcomb_bits())) != hipSuccess) return NT_ENOMEM;
+      NT_CHK0(build_wcombs(nt::bcomb_bits(), kB, 1, 0, d_combB, nullptr));
     }
     // Workspace slots = grid cap of the verify kernel.  Four times the resident
     // workgroups (256-thread blocks, `occupancy` waves per SIMD, 4 SIMDs per CU):
@@ -168,17 +168,17 @@ struct Device {
 
   // Wide combs of nkeys encoded points (host words) into d_comb (device);
   // negate: comb of -P (committee keys) instead of P (the base point).
-  int build_wcombs(const uint32_t* enc_host, uint32_t nkeys, int negate, uint32_t* d_comb, uint32_t* d_meta) {
+  int build_wcombs(int bits, const uint32_t* enc_host, uint32_t nkeys, int negate, uint32_t* d_comb, uint32_t* d_meta) {
     if (nkeys == 0) return NT_OK;
-    const uint32_t batch = std::min<uint32_t>(nkeys, 16);
+    const uint32_t batch = std::min<uint32_t>(nkeys, nt::wcomb_fill_batch(bits));
     uint32_t *d_enc = nullptr, *d_bases = nullptr, *d_tmp = nullptr;
     int rc = NT_OK;
     if (hipMalloc(&d_enc, 32ull * nkeys) != hipSuccess ||
-        hipMalloc(&d_bases, nt::wcomb_bases_bytes_per_key() * nkeys) != hipSuccess ||
-        hipMalloc(&d_tmp, nt::wcomb_fill_tmp_bytes_per_key() * batch) != hipSuccess) {
+        hipMalloc(&d_bases, nt::wcomb_bases_bytes_per_key(bits) * nkeys) != hipSuccess ||
+        hipMalloc(&d_tmp, nt::wcomb_fill_tmp_bytes_per_key(bits) * batch) != hipSuccess) {
       rc = NT_ENOMEM;
     } else if (hipMemcpyAsync(d_enc, enc_host, 32ull * nkeys, hipMemcpyHostToDevice, stream) != hipSuccess ||
-               nt::launch_wcomb_build(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, stream) !=
+               nt::launch_wcomb_build(bits, d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, stream) !=
                    hipSuccess ||
                hipStreamSynchronize(stream) != hipSuccess) {
       rc = NT_EHIP;
@@ -243,6 +243,7 @@ struct nt_ctx {
 struct nt_keyset {
   nt_ctx* ctx = nullptr;
   uint32_t nkeys = 0;
+  int bits = 0;                 // comb digit width of every key (nt::kKeyCombWide / kKeyCombNarrow)
   std::vector<uint32_t> flags;  // host copy of kKey* bits
   struct PerDev {
     int ordinal = -1;
@@ -793,7 +794,7 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
                                      (uint64_t*)doff, (uint64_t*)dlen, s));
         if (ks) {
           const auto& pd = *(const nt_keyset::PerDev*)pd_meta;
-          NT_TRY(nt::launch_verify_keyset(NT_MODE_COFACTORLESS, (const uint32_t*)dk, dsig, dmsg, doff, dlen, mc,
+          NT_TRY(nt::launch_verify_keyset(NT_MODE_COFACTORLESS, ks->bits, (const uint32_t*)dk, dsig, dmsg, doff, dlen, mc,
                                           pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB,
                                           (c & 1) ? dv.stash2.p : dv.d[B_STASH].p, dout, s));
         } else {
@@ -877,12 +878,31 @@ int nt_ed25519_keypair_batch(nt_ctx* ctx, const uint8_t* seed32, uint64_t n, uin
 }
 
 // ---- committee key cache --------------------------------------------------
+// Comb width of a new key set: 20-bit combs (13 additions per [k]A, 872 MB per
+// key) when every device can hold them and keep 1/8 of its HBM free, else
+// 16-bit combs (16 additions, 67 MB per key).  NT_KEYSET_COMB_BITS=16|20 forces one.
+static int keyset_comb_bits(nt_ctx* ctx, uint32_t nkeys) {
+  if (const char* e = std::getenv("NT_KEYSET_COMB_BITS")) {
+    const int b = std::atoi(e);
+    if (b == nt::kKeyCombWide || b == nt::kKeyCombNarrow) return b;
+  }
+  const size_t need = nt::wcomb_bytes_per_key(nt::kKeyCombWide) * std::max<uint32_t>(nkeys, 1) +
+                      nt::wcomb_fill_tmp_bytes_per_key(nt::kKeyCombWide) * nt::wcomb_fill_batch(nt::kKeyCombWide);
+  for (auto& d : ctx->devs) {
+    size_t fr = 0, tot = 0;
+    if (hipSetDevice(d->ordinal) != hipSuccess || hipMemGetInfo(&fr, &tot) != hipSuccess) return nt::kKeyCombNarrow;
+    if (fr < need + tot / 8) return nt::kKeyCombNarrow;
+  }
+  return nt::kKeyCombWide;
+}
+
 int nt_keyset_create(nt_ctx* ctx, const uint8_t* pk32, uint32_t nkeys, nt_keyset** out) {
   if (!ctx || !out || (nkeys && !pk32)) return NT_EINVAL;
   *out = nullptr;
   auto ks = std::make_unique<nt_keyset>();
   ks->ctx = ctx;
   ks->nkeys = nkeys;
+  ks->bits = keyset_comb_bits(ctx, nkeys);
   ks->flags.assign(nkeys, 0);
   ks->dev.resize(ctx->devs.size());
   for (size_t di = 0; di < ctx->devs.size(); ++di) {
@@ -894,11 +914,11 @@ int nt_keyset_create(nt_ctx* ctx, const uint8_t* pk32, uint32_t nkeys, nt_keyset
     const size_t nk = std::max<uint32_t>(nkeys, 1);
     if (hipMalloc(&pd.d_enc, 32 * nk) != hipSuccess) return NT_ENOMEM;
     if (hipMalloc(&pd.d_meta, 4 * nk) != hipSuccess) return NT_ENOMEM;
-    if (hipMalloc(&pd.d_comb, nt::wcomb_bytes_per_key() * nk) != hipSuccess) return NT_ENOMEM;
+    if (hipMalloc(&pd.d_comb, nt::wcomb_bytes_per_key(ks->bits) * nk) != hipSuccess) return NT_ENOMEM;
     if (nkeys) {
       NT_TRY(hipMemcpyAsync(pd.d_enc, pk32, 32ull * nkeys, hipMemcpyHostToDevice, dv.stream));
       NT_TRY(hipStreamSynchronize(dv.stream));
-      const int rc = dv.build_wcombs((const uint32_t*)pk32, nkeys, 1, pd.d_comb, pd.d_meta);
+      const int rc = dv.build_wcombs(ks->bits, (const uint32_t*)pk32, nkeys, 1, pd.d_comb, pd.d_meta);
       if (rc != NT_OK) return rc;
       if (di == 0)
         NT_TRY(hipMemcpyAsync(ks->flags.data(), pd.d_meta, 4ull * nkeys, hipMemcpyDeviceToHost, dv.stream));
@@ -917,6 +937,14 @@ int nt_keyset_flags(const nt_keyset* ks, uint32_t i, uint32_t* flags) {
   return NT_OK;
 }
 
+
+int nt_keyset_info(const nt_keyset* ks, uint32_t* comb_bits, uint64_t* bytes_per_device) {
+  if (!ks) return NT_EINVAL;
+  const uint64_t nk = std::max<uint32_t>(ks->nkeys, 1);
+  if (comb_bits) *comb_bits = (uint32_t)ks->bits;
+  if (bytes_per_device) *bytes_per_device = (nt::wcomb_bytes_per_key(ks->bits) + 36) * nk;
+  return NT_OK;
+}
 
 int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const uint32_t* key_idx,
                              const uint8_t* sig64, const uint8_t* msg, const uint64_t* off,
@@ -946,7 +974,7 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
       NT_TRY(hipMemcpyAsync(dv.d[B_SIG].as<uint8_t>() + 64 * a, sig64 + 64 * (lo + a), (b - a) * 64,
                             hipMemcpyHostToDevice, dv.cstream));
       NT_TRY(dv.fence((int)c));
-      NT_TRY(nt::launch_verify_keyset(mode, dv.d[B_PK].as<uint32_t>() + a, dv.d[B_SIG].as<uint8_t>() + 64 * a,
+      NT_TRY(nt::launch_verify_keyset(mode, ks->bits, dv.d[B_PK].as<uint32_t>() + a, dv.d[B_SIG].as<uint8_t>() + 64 * a,
                                       dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>() + a,
                                       dv.d[B_LEN].as<uint64_t>() + a, b - a, pd.d_meta, pd.d_enc, pd.d_comb,
                                       ks->nkeys, dv.d_combB, (c & 1) ? dv.stash2.p : dv.d[B_STASH].p,
@@ -1024,7 +1052,7 @@ int nt_dev_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int dev, void
     NT_CHK(dv->d[B_STASH].ensure(nt::keyset_stash_bytes(n)));
     stash = dv->d[B_STASH].p;
   }
-  NT_TRY(nt::launch_verify_keyset(mode, d_key_idx, d_sig64, d_msg, d_off, d_len, n, pd.d_meta, pd.d_enc, pd.d_comb,
+  NT_TRY(nt::launch_verify_keyset(mode, ks->bits, d_key_idx, d_sig64, d_msg, d_off, d_len, n, pd.d_meta, pd.d_enc, pd.d_comb,
                                   ks->nkeys, dv->d_combB, stash, d_out_words, s));
   return NT_OK;
 }

@@ -26,7 +26,7 @@ EXPORTED = [
     "nt_sha512_trunc32", "nt_ed25519_verify_strict", "nt_ed25519_verify_batch_groups",
     "nt_ed25519_sign_batch", "nt_ed25519_keypair_batch", "nt_dev_sha512_trunc32",
     "nt_dev_ed25519_verify", "nt_dev_group_and", "nt_dev_ed25519_sign", "nt_keyset_create",
-    "nt_keyset_free", "nt_keyset_flags", "nt_ed25519_verify_keyset", "nt_ed25519_verify_batch_groups_keyset",
+    "nt_keyset_free", "nt_keyset_flags", "nt_keyset_info", "nt_ed25519_verify_keyset", "nt_ed25519_verify_batch_groups_keyset",
     "nt_dev_ed25519_verify_keyset", "nt_host_alloc", "nt_host_free",
 ]
 
@@ -73,6 +73,7 @@ def load_library(path=None):
     lib.nt_keyset_free.argtypes = [_vp]
     lib.nt_keyset_free.restype = None
     lib.nt_keyset_flags.argtypes = [_vp, ctypes.c_uint32, _u32p]
+    lib.nt_keyset_info.argtypes = [_vp, _u32p, _u64p]
     lib.nt_ed25519_verify_keyset.argtypes = [_vp, _vp, ctypes.c_int, _u32p, _u8p, _u8p, _u64p, _u64p, _u64, _u8p]
     lib.nt_ed25519_verify_batch_groups_keyset.argtypes = [_vp, _vp, _u32p, _u8p, _u64p, _u32p, _u8p, _u64, _u8p,
                                                           _u8p]
@@ -245,6 +246,12 @@ class Keyset:
         f = ctypes.c_uint32()
         _check(self.be.lib.nt_keyset_flags(self.h, i, ctypes.byref(f)), "nt_keyset_flags")
         return int(f.value)
+
+    def info(self):
+        """(comb digit width, device bytes per device) -- nt_keyset_info"""
+        b, nb = ctypes.c_uint32(), ctypes.c_uint64()
+        _check(self.be.lib.nt_keyset_info(self.h, ctypes.byref(b), ctypes.byref(nb)), "nt_keyset_info")
+        return int(b.value), int(nb.value)
 
     def verify(self, mode, key_idx, sig, msg, off, ln):
         key_idx = np.ascontiguousarray(key_idx, np.uint32)

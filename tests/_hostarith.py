@@ -111,12 +111,13 @@ def sc_halfsize(k: int):
     return (-uu if neg.value else uu), int.from_bytes(v.raw, "little"), bits
 
 
-def wcomb_chunk(enc, negate, pos, c):
+def wcomb_chunk(bits, enc, negate, pos, c):
     """Device wide-comb construction on the host: (meta, 65 x 32 words) for
-    entries 64c .. 64c+64 of position pos (entry 64c only filled when c == 0)."""
+    entries 64c .. 64c+64 of position pos of the `bits`-bit comb (entry 64c only
+    filled when c == 0)."""
     import numpy as np
     out = (ctypes.c_uint32 * (65 * 32))()
-    meta = load().nth_wcomb_chunk(enc, negate, pos, c, out)
+    meta = load().nth_wcomb_chunk(bits, enc, negate, pos, c, out)
     return meta, np.frombuffer(bytes(out), np.uint32).reshape(65, 32)
 
 

@@ -28,14 +28,16 @@ struct HostATab {
 
 // Wide comb of a point with entries computed on demand (and memoized) by
 // plain double-and-add; table construction is not counted by NT_OPCOUNT.
+template <int W>
 struct HostWComb {
-  ge_p3 base[kWPos];
-  mutable std::unordered_map<uint32_t, ge_niels> memo;
+  static constexpr int kBits = W;
+  ge_p3 base[CombGeom<W>::kPos];
+  mutable std::unordered_map<uint64_t, ge_niels> memo;
   void init(const ge_p3& P) {
     const unsigned long long m0 = g_fe_mul, s0 = g_fe_sq;
-    uint32_t w[kWPos * 40];
-    wcomb_bases(w, P);
-    for (int i = 0; i < kWPos; ++i)
+    uint32_t w[CombGeom<W>::kPos * 40];
+    wcomb_bases<W>(w, P);
+    for (int i = 0; i < CombGeom<W>::kPos; ++i)
       for (int l = 0; l < 10; ++l) {
         base[i].X.v[l] = w[40 * i + l];
         base[i].Y.v[l] = w[40 * i + 10 + l];
@@ -46,7 +48,7 @@ struct HostWComb {
     g_fe_sq = s0;
   }
   void load(uint32_t pos, uint32_t idx, ge_niels& q) const {
-    const uint32_t key = (pos << 16) | idx;
+    const uint64_t key = ((uint64_t)pos << 32) | idx;
     auto it = memo.find(key);
     if (it != memo.end()) {
       q = it->second;
@@ -61,7 +63,7 @@ struct HostWComb {
       ge_p3 Q;
       ge_p3_0(Q);
       ge_cp t;
-      for (int bit = 15; bit >= 0; --bit) {
+      for (int bit = W - 1; bit >= 0; --bit) {
         ge_p2 q2;
         ge_p3_to_p2(q2, Q);
         ge_dbl(t, q2);
@@ -81,9 +83,12 @@ struct HostWComb {
   }
 };
 
-HostWComb& bcomb() {
-  static HostWComb* c = [] {
-    auto* w = new HostWComb;
+using HostBComb = HostWComb<kBCombBits>;
+using HostKeyComb = HostWComb<kKeyCombWide>;  // the device's choice whenever the set fits in HBM
+
+HostBComb& bcomb() {
+  static HostBComb* c = [] {
+    auto* w = new HostBComb;
     uint32_t enc[8];
     for (int i = 0; i < 8; ++i) enc[i] = kBaseEnc[i];
     ge_p3 B;
@@ -95,7 +100,7 @@ HostWComb& bcomb() {
 }
 
 // kKey* bits and the comb of -A, as k_wcomb_bases builds them
-uint32_t key_comb(HostWComb& c, const uint32_t Aw[8]) {
+uint32_t key_comb(HostKeyComb& c, const uint32_t Aw[8]) {
   ge_p3 P;
   const uint32_t ok = ge_frombytes_w(P, Aw);
   const uint32_t meta = (ok ? kKeyDecodes : 0u) | (ge_is_small_order(P) ? kKeySmallOrder : 0u);
@@ -236,7 +241,8 @@ struct HostStash {
   void get_prefix(int j, fe& a) const { a = pre[j]; }
 };
 struct HostCombRef {  // a comb by reference, with the WComb interface
-  const HostWComb* c;
+  static constexpr int kBits = HostKeyComb::kBits;
+  const HostKeyComb* c;
   void load(uint32_t pos, uint32_t idx, ge_niels& q) const { c->load(pos, idx, q); }
 };
 struct HostLoader {
@@ -246,7 +252,7 @@ struct HostLoader {
   const uint8_t* const* M;
   const uint64_t* L;
   const uint32_t* meta;
-  HostWComb* ca;
+  HostKeyComb* ca;
   void get(int j, uint32_t& m, uint32_t Aw[8], uint32_t Rw[8], uint32_t Sw[8], const uint8_t*& msg, uint64_t& len,
            Comb& c) const {
     m = meta[j];
@@ -265,7 +271,7 @@ int nth_verify_cached_n(int mode, int nsig, const uint8_t* pk, const uint8_t* si
   alignas(16) uint32_t A[4][8], S[4][16];
   std::memcpy(A, pk, 32 * nsig);
   std::memcpy(S, sig, 64 * nsig);
-  static HostWComb ca[4];
+  static HostKeyComb ca[4];
   const unsigned long long cm = g_fe_mul, cs = g_fe_sq;  // key-cache build is not per signature
   uint32_t meta[4];
   for (int j = 0; j < nsig; ++j) {
@@ -301,7 +307,7 @@ void nth_sign(const uint8_t* seed, const uint8_t* msg, uint64_t len, uint8_t* pk
 // The device's wide-comb construction run on the host for one chunk: entries
 // j0-1 .. j0+63 (j0 = 1 + 64c; entry j0-1 only written for c = 0) of position
 // pos of the comb of P (negate: of -P), as 65 x 32 words.  Returns kKey* bits.
-uint32_t nth_wcomb_chunk(const uint8_t* enc32, int negate, int pos, int c, uint32_t* out) {
+uint32_t nth_wcomb_chunk(int bits, const uint8_t* enc32, int negate, int pos, int c, uint32_t* out) {
   uint32_t w[8];
   words(w, enc32);
   ge_p3 P;
@@ -314,11 +320,18 @@ uint32_t nth_wcomb_chunk(const uint8_t* enc32, int negate, int pos, int c, uint3
     fe_neg(P.T, P.T);
     fe_carry(P.T);
   }
-  static uint32_t bases[kWPos * 40];
-  wcomb_bases(bases, P);
+  static uint32_t bases[CombGeom<kKeyCombNarrow>::kPos * 40];
   static uint32_t tmp[kWChunk * 10];
   std::memset(out, 0, 65 * kWStride * 4);
-  wcomb_fill(out + kWStride, tmp, bases + 40 * pos, (uint32_t)c);
+  if (bits == kKeyCombWide) {
+    wcomb_bases<kKeyCombWide>(bases, P);
+    wcomb_fill<kKeyCombWide>(out + kWStride, tmp, bases + 40 * pos, (uint32_t)c);
+  } else if (bits == kKeyCombNarrow) {
+    wcomb_bases<kKeyCombNarrow>(bases, P);
+    wcomb_fill<kKeyCombNarrow>(out + kWStride, tmp, bases + 40 * pos, (uint32_t)c);
+  } else {
+    return ~0u;
+  }
   return meta;
 }
 void nth_counts_reset() { bcomb(); g_fe_mul = g_fe_sq = 0; }

@@ -212,20 +212,42 @@ def test_batch_corpus_rule(be, corpus):
 
 
 # ------------------------------------------------------------------ committee key cache
-def test_keyset_corpus(be, corpus):
-    """Every corpus key (incl. off-curve, small-order, non-canonical) as a keyset entry."""
-    ks = be.keyset(corpus["pk"])
-    n = len(corpus["pk"])
-    idx = np.arange(n, dtype=np.uint32)
+@pytest.mark.parametrize("bits", [16, 20])
+def test_keyset_corpus(be, corpus, bits, monkeypatch):
+    """Every corpus key (incl. off-curve, small-order, non-canonical) as a keyset
+    entry, through both key-comb widths (NT_KEYSET_COMB_BITS forces one; the
+    20-bit combs take 872 MB per key, so those sets hold 48 keys at a time)."""
     import ntcrypto
-    got_s = ks.verify(ntcrypto.NT_MODE_STRICT, idx, corpus["sig"], corpus["msg"], corpus["off"], corpus["len"])
+    monkeypatch.setenv("NT_KEYSET_COMB_BITS", str(bits))
+    uniq, inv = np.unique(corpus["pk"], axis=0, return_inverse=True)
+    inv = inv.ravel().astype(np.uint32)
+    per_set = len(uniq) if bits == 16 else 48
+    n = len(corpus["pk"])
+    got_s = np.zeros(n, bool)
+    got_c = np.zeros(n, bool)
+    for k0 in range(0, len(uniq), per_set):
+        ks = be.keyset(uniq[k0:k0 + per_set])
+        assert ks.info()[0] == bits
+        sel = np.nonzero((inv >= k0) & (inv < k0 + per_set))[0]
+        idx = inv[sel] - k0
+        args = (corpus["sig"][sel], corpus["msg"], corpus["off"][sel], corpus["len"][sel])
+        got_s[sel] = ks.verify(ntcrypto.NT_MODE_STRICT, idx, *args)
+        got_c[sel] = ks.verify(ntcrypto.NT_MODE_COFACTORLESS, idx, *args)
+        # unknown key index -> reject
+        assert not ks.verify(ntcrypto.NT_MODE_STRICT, np.full(len(sel), per_set + 5, np.uint32), *args).any()
+        ks.close()
     assert np.array_equal(got_s, corpus["strict"].astype(bool))
-    got_c = ks.verify(ntcrypto.NT_MODE_COFACTORLESS, idx, corpus["sig"], corpus["msg"], corpus["off"], corpus["len"])
     assert np.array_equal(got_c, corpus["batch_rule"].astype(bool))
-    # unknown key index -> reject
-    bad = ks.verify(ntcrypto.NT_MODE_STRICT, np.full(n, n + 5, np.uint32), corpus["sig"], corpus["msg"],
-                    corpus["off"], corpus["len"])
-    assert not bad.any()
+
+
+def test_keyset_comb_width_choice(be):
+    """Without an override a committee that fits gets 20-bit combs; the size
+    nt_keyset_info reports is the comb bytes of every key."""
+    pks = be.sign_batch(np.arange(4 * 32, dtype=np.uint8).reshape(4, 32))
+    ks = be.keyset(pks)
+    bits, nbytes = ks.info()
+    assert bits == 20
+    assert nbytes >= 4 * 13 * ((1 << 19) + 1) * 128
     ks.close()
 
 

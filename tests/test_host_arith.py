@@ -183,18 +183,24 @@ def _model():
     return mod
 
 
-def test_wide_comb_construction_vs_model():
-    """wcomb_bases + wcomb_fill (the device build of j * 2^(16 i) * P, affine niels
-    with one batched inversion per chunk) against the textbook model."""
+@pytest.mark.parametrize("bits", [20, 16])
+def test_wide_comb_construction_vs_model(bits):
+    """wcomb_bases + wcomb_fill (the device build of j * 2^(W i) * P, affine niels
+    with one batched inversion per chunk) against the textbook model, for both
+    comb widths the device builds (20-bit: B and committee keys that fit in HBM;
+    16-bit: committee keys otherwise): first, second and last position, first,
+    second and last chunk."""
     M = _model()
     with open(os.path.join(GOLD, "fixtures_reference.json")) as f:
         pk = bytes.fromhex(json.load(f)["keys"][1]["pk"])
+    npos = (254 + bits - 1) // bits
+    last_chunk = (1 << (bits - 1)) // 64 - 1
     cases = [(M.encode(M.BASE), 0, M.BASE), (pk, 1, M.pneg(M.decode(pk)))]
     for enc, neg, pt in cases:
-        for pos in (0, 1, 15):
-            base = M.pmul(2 ** (16 * pos), pt)
-            for c in (0, 1, 511):
-                meta, e = H.wcomb_chunk(enc, neg, pos, c)
+        for pos in (0, 1, npos - 1):
+            base = M.pmul(2 ** (bits * pos), pt)
+            for c in (0, 1, last_chunk):
+                meta, e = H.wcomb_chunk(bits, enc, neg, pos, c)
                 assert meta == 1
                 q = M.pmul(64 * c, base)
                 for idx in range(65):
