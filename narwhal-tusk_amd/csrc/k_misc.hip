@@ -62,14 +62,20 @@ struct KwLdsSink {
     slot[P * 64 + lane] = make_uint4((uint32_t)kw0, (uint32_t)(kw0 >> 32), (uint32_t)kw1, (uint32_t)(kw1 >> 32));
   }
 };
-struct KwLdsSource {
-  const uint4* slot;
-  uint32_t lane;
+// The consumer keeps kKwAhead LDS reads in flight: consuming pair P issues the
+// read of pair P + kKwAhead, so each read has ~2 kKwAhead rounds of work to
+// land in and the wait before a round is (almost) never a stall.  (Reading a
+// pair only when its rounds start left ~100 cycles of LDS latency per 4
+// rounds; reading all 40 up front makes one wait for 40 KB per block.)
+constexpr int kKwAhead = 12;  // <= 15: the lgkmcnt counter tracks every read in flight
+struct KwPrefetchSource {
+  const uint4* lds;  // this lane's pair 0 in the ring slot (pairs 64 uint4 apart)
+  uint4* q;          // [40] registers
   template <int P>
   NT_D NT_INLINE void get(uint64_t& kw0, uint64_t& kw1) const {
-    const uint4 q = slot[P * 64 + lane];
-    kw0 = ((uint64_t)q.y << 32) | q.x;
-    kw1 = ((uint64_t)q.w << 32) | q.z;
+    if constexpr (P + kKwAhead < 40) q[P + kKwAhead] = lds[(P + kKwAhead) * 64];
+    kw0 = ((uint64_t)q[P].y << 32) | q[P].x;
+    kw1 = ((uint64_t)q[P].w << 32) | q[P].z;
   }
 };
 
@@ -127,7 +133,11 @@ __global__ __launch_bounds__(128) void k_sha512_pipe(const uint8_t* __restrict__
         uint64_t v[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = st[q];
-        const KwLdsSource src{ring[b & 1], lane};
+        uint4 q[40];
+        const uint4* lds = ring[b & 1] + lane;
+#pragma unroll
+        for (int p = 0; p < kKwAhead; ++p) q[p] = lds[p * 64];
+        const KwPrefetchSource src{lds, q};
         sha_rounds_kw<0>(v, src);
         const bool upd = b < nblocks;
 #pragma unroll
