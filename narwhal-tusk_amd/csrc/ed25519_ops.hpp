@@ -335,11 +335,11 @@ NT_HD NT_INLINE void hram_scalar(uint32_t k[8], const uint32_t Rw[8], const uint
 // anyway).  verify_cached_batch gets the N Z^-1 of a lane from one inversion
 // (Montgomery's trick).
 // ---------------------------------------------------------------------------
-NT_HD NT_INLINE uint32_t enc_matches(const fe& x, const fe& y, const uint32_t Rw[8]) {
+// a = canonical words of y'
+NT_HD NT_INLINE uint32_t enc_matches(const fe& x, const uint32_t a[8], const uint32_t Rw[8]) {
   fe yr;
   fe_frombytes_w(yr, Rw);  // bit 255 dropped, value taken mod p by the compare
-  uint32_t a[8], b[8], xw[8];
-  fe_tobytes_w(a, y);
+  uint32_t b[8], xw[8];
   fe_tobytes_w(b, yr);
   fe_tobytes_w(xw, x);
   uint32_t same = 1, xz = 0;
@@ -363,13 +363,13 @@ NT_HD NT_INLINE uint32_t verify_uv(const uint32_t Aw[8], const uint32_t Rw[8], c
   {
     ge_p3 A;
     ok &= ge_frombytes_w(A, Aw);
-    if (MODE == kStrict) ok &= ge_is_small_order(A) ^ 1u;
+    if (MODE == kStrict) ok &= ge_is_small_order_affine(A) ^ 1u;
     ptab_build(A, uneg ^ 1u, at, 0);  // -[u]A = [|u|](u < 0 ? A : -A)
   }
   {
     ge_p3 R;
     ok &= ge_frombytes_w(R, Rw);
-    if (MODE == kStrict) ok &= ge_is_small_order(R) ^ 1u;
+    if (MODE == kStrict) ok &= ge_is_small_order_affine(R) ^ 1u;
     ptab_build(R, 1u, at, kTabR);
   }
   uint32_t w[8], ud[8], vd[8];
@@ -448,8 +448,10 @@ NT_HD NT_INLINE uint32_t compare_one(const ge_p2& P, const fe& zi, const uint32_
   fe x, y;
   fe_mul(x, P.X, zi);
   fe_mul(y, P.Y, zi);
-  uint32_t r = enc_matches(x, y, Rw);
-  if (MODE == kStrict) r &= ge_is_small_order_p2(P) ^ 1u;
+  uint32_t yw[8];
+  fe_tobytes_w(yw, y);
+  uint32_t r = enc_matches(x, yw, Rw);
+  if (MODE == kStrict) r &= torsion_y_words(yw) ^ 1u;  // R' on the curve: small order <=> torsion y
   return r;
 }
 

@@ -222,7 +222,32 @@ NT_HD NT_INLINE uint32_t ge_p2_is_identity(const ge_p2& p) {
   return fe_iszero(p.X) & fe_eq(p.Y, p.Z);
 }
 
-// [8]P == identity  (EdwardsPoint::is_small_order)
+// Small order from the canonical y alone: the 8 torsion points are exactly the
+// curve points with y in {1, -1, 0, +-y8} (identity, order 2, the two of
+// order 4, the four of order 8 -- and -(x, y) = (-x, y) keeps the set closed),
+// so for a point ON the curve "[8]P == identity" (EdwardsPoint::is_small_order)
+// is 5 word compares instead of 3 doublings.  y = canonical words (< p).
+NT_HD NT_INLINE uint32_t torsion_y_words(const uint32_t y[8]) {
+  uint32_t z = 1, one = 1, m1 = 1, a = 1, b = 1;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t pm1 = i == 0 ? 0xffffffecu : (i == 7 ? 0x7fffffffu : 0xffffffffu);  // p - 1
+    z &= y[i] == 0u;
+    one &= y[i] == (i == 0 ? 1u : 0u);
+    m1 &= y[i] == pm1;
+    a &= y[i] == kTorsionY8[i];
+    b &= y[i] == kTorsionY8n[i];
+  }
+  return z | one | m1 | a | b;
+}
+// small order of a decoded point (ge_frombytes_w: Z = 1, Y = y, possibly >= p)
+NT_HD NT_INLINE uint32_t ge_is_small_order_affine(const ge_p3& p) {
+  uint32_t w[8];
+  fe_tobytes_w(w, p.Y);
+  return torsion_y_words(w);
+}
+
+// [8]P == identity  (EdwardsPoint::is_small_order), by doublings: any Z
 NT_HD NT_INLINE uint32_t ge_is_small_order_p2(const ge_p2& p) {
   ge_p2 t = p;
 #pragma unroll 1

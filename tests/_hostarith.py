@@ -111,6 +111,13 @@ def sc_halfsize(k: int):
     return (-uu if neg.value else uu), int.from_bytes(v.raw, "little"), bits
 
 
+def small_order(enc):
+    """(decodes, [8]P == 0 by doublings, torsion-y compare) for a 32-byte encoding"""
+    a, b = ctypes.c_int(0), ctypes.c_int(0)
+    ok = load().nth_small_order(enc, ctypes.byref(a), ctypes.byref(b))
+    return bool(ok), bool(a.value), bool(b.value)
+
+
 def wcomb_chunk(bits, enc, negate, pos, c):
     """Device wide-comb construction on the host: (meta, 65 x 32 words) for
     entries 64c .. 64c+64 of position pos of the `bits`-bit comb (entry 64c only

@@ -334,6 +334,17 @@ uint32_t nth_wcomb_chunk(int bits, const uint8_t* enc32, int negate, int pos, in
   }
   return meta;
 }
+// small-order test of a decodable encoding both ways: [8]P by doublings and
+// the torsion-y compare the kernels use; returns decode ok
+int nth_small_order(const uint8_t* enc32, int* by_dbl, int* by_y) {
+  uint32_t w[8];
+  words(w, enc32);
+  ge_p3 P;
+  const uint32_t ok = ge_frombytes_w(P, w);
+  *by_dbl = (int)ge_is_small_order(P);
+  *by_y = (int)ge_is_small_order_affine(P);
+  return (int)ok;
+}
 void nth_counts_reset() { bcomb(); g_fe_mul = g_fe_sq = 0; }
 unsigned long long nth_count_mul() { return g_fe_mul; }
 unsigned long long nth_count_sq() { return g_fe_sq; }

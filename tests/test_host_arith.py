@@ -183,6 +183,28 @@ def _model():
     return mod
 
 
+def test_small_order_by_torsion_y():
+    """The kernels' small-order test (y in {1, -1, 0, +-y8}) equals [8]P == 0 by
+    doublings (and the textbook model) on every small-order encoding the corpus
+    uses -- canonical, non-canonical (y + p) and negative-zero forms -- on
+    mixed-order points T + aB and on random points."""
+    M = _model()
+    encs = list(M.small_order_encodings()) + [M.encode(t) for t in M.TORSION]
+    rng = random.Random(5)
+    for t in M.TORSION:
+        for _ in range(3):
+            encs.append(M.encode(M.padd(t, M.pmul(rng.randrange(1, M.L), M.BASE))))
+    encs += [M.encode(M.pmul(rng.randrange(1, M.L), M.BASE)) for _ in range(20)]
+    n_small = 0
+    for e in encs:
+        ok, by_dbl, by_y = H.small_order(e)
+        assert ok == (M.decode(e) is not None)
+        if ok:
+            assert by_dbl == by_y == M.is_small(M.decode(e)), e.hex()
+            n_small += by_y
+    assert n_small >= 8
+
+
 @pytest.mark.parametrize("bits", [20, 16])
 def test_wide_comb_construction_vs_model(bits):
     """wcomb_bases + wcomb_fill (the device build of j * 2^(W i) * P, affine niels
