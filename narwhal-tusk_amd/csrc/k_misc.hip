@@ -19,11 +19,11 @@
 //
 // SIMT design: every lane runs the same window schedule (fixed signed windows,
 // a wave-uniform window count, never per-lane sliding windows), so lanes of a
-// wave never diverge inside the scalar multiplications.  [v s]B is 16 mixed
-// additions from the 67 MB wide comb of B (random 128-byte lines, the next one
-// prefetched during the current addition); [u](+-A) + [v](-R) use joint 4-bit
-// windows over per-lane 9-entry cached tables in a global workspace laid out
-// lane-minor so each lane's 16-byte accesses coalesce across the workgroup.
+// wave never diverge inside the scalar multiplications.  [v s]B is 13 mixed
+// additions from the 872 MB 20-bit wide comb of B (random 128-byte lines, the
+// next one prefetched during the current addition); [u](+-A) + [v](-R) use
+// joint 4-bit windows over per-lane 9-entry cached tables in a global
+// workspace laid out lane-major, so a lookup's loads use whole lines.
 #include "kernels_common.hpp"
 
 namespace nt {

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Summarize tools/pmc_collect.sh output into a per-launch JSON for profiles/.
 
-Per kernel: counters summed over its dispatches and divided by the dispatch
-count (per launch).  HBM traffic per launch = FETCH_SIZE*1024*2 (gfx950 reports
+Per (kernel, grid size): counters summed over its dispatches and divided by
+the dispatch count (per launch).  HBM traffic per launch = FETCH_SIZE*1024*2 (gfx950 reports
 half the bytes of wide 16-B/lane streaming reads; MI355X_MICROARCH.md §HBM) +
 WRITE_SIZE*1024; the uncorrected read figure is kept beside it.
 VALU issue share = SQ_INSTS_VALU * 4 cycles / (SIMDs * GRBM_GUI_ACTIVE/8).
@@ -25,7 +25,23 @@ def kname(k):
     return None
 
 
+def _derive(c, nd):
+    per = {k: v / nd for k, v in c.items()}
+    d = {"dispatches_per_pass": nd, "per_launch": per}
+    if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
+        d["hbm_bytes_per_launch"] = per["FETCH_SIZE"] * 1024 * 2 + per["WRITE_SIZE"] * 1024
+        d["hbm_bytes_per_launch_uncorrected"] = (per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024
+    if "SQ_INSTS_VALU" in per and "GRBM_GUI_ACTIVE" in per:
+        cyc = per["GRBM_GUI_ACTIVE"] / 8
+        d["valu_issue_share_4cyc"] = per["SQ_INSTS_VALU"] * 4 / (1024 * cyc)
+    return d
+
+
 def main(indir, out, tag):
+    """Counters per (kernel, grid size): one bench command launches a kernel for
+    several workloads (e.g. the verify kernel for config 2's 1M signatures and in
+    chunks for the host entry points).  "kernels" reports each kernel's
+    LARGEST-grid launches (the config's resident-data launch); "by_grid" all."""
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(lambda: collections.defaultdict(set))
     for f in sorted(glob.glob(os.path.join(indir, "pass*", "*counter_collection.csv"))):
@@ -34,23 +50,20 @@ def main(indir, out, tag):
             n = kname(r["Kernel_Name"])
             if not n:
                 continue
-            acc[n][r["Counter_Name"]] += float(r["Counter_Value"])
-            disp[n][pdir].add(r["Dispatch_Id"])
-    res = {"tag": tag, "source": indir, "kernels": {}}
-    for n, c in acc.items():
-        nd = max(len(v) for v in disp[n].values())
-        per = {k: v / nd for k, v in c.items()}
-        d = {"dispatches_per_pass": nd, "per_launch": per}
-        if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
-            d["hbm_bytes_per_launch"] = per["FETCH_SIZE"] * 1024 * 2 + per["WRITE_SIZE"] * 1024
-            d["hbm_bytes_per_launch_uncorrected"] = (per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024
-        if "SQ_INSTS_VALU" in per and "GRBM_GUI_ACTIVE" in per:
-            cyc = per["GRBM_GUI_ACTIVE"] / 8
-            d["valu_issue_share_4cyc"] = per["SQ_INSTS_VALU"] * 4 / (1024 * cyc)
-        res["kernels"][n] = d
+            key = (n, int(r["Grid_Size"]))
+            acc[key][r["Counter_Name"]] += float(r["Counter_Value"])
+            disp[key][pdir].add(r["Dispatch_Id"])
+    res = {"tag": tag, "source": indir, "kernels": {}, "by_grid": {}}
+    for (n, g), c in sorted(acc.items()):
+        nd = max(len(v) for v in disp[(n, g)].values())
+        d = _derive(c, nd)
+        d["grid"] = g
+        res["by_grid"]["%s@%d" % (n, g)] = d
+        if n not in res["kernels"] or g > res["kernels"][n]["grid"]:
+            res["kernels"][n] = d
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
-    print(json.dumps(res, indent=1)[:3000])
+    print(json.dumps(res["kernels"], indent=1)[:3000])
 
 
 if __name__ == "__main__":
