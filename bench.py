@@ -41,7 +41,7 @@ sys.path.insert(0, os.path.join(ROOT, "narwhal-tusk_amd"))
 METRIC = "Ed25519 verifies/sec + SHA-512 GB/s at 1/2/4/8 MI355X vs dalek host-core base"
 MAD_PEAK_TS = 256 * 4 * 64 * 2.4e9 / 4 / 1e12  # v_mad_u64_u32: 4 cycles per wave64 per SIMD
 HBM_PEAK_GBS = 8000.0
-PMC_PROFILE = os.path.join("r01", "pmc_v6.json")  # tools/profile_round.sh + tools/pmc_summarize.py
+PMC_PROFILE = os.path.join("r01", "pmc_v8.json")  # tools/profile_round.sh + tools/pmc_summarize.py
 PMC_N = 1_000_000  # signatures per launch in that profile (the default config-2 run)
 SODIUM = "/opt/conda/lib/libsodium.so.23"
 
@@ -184,8 +184,10 @@ def main():
                 "frac": round(achieved / MAD_PEAK_TS, 4),
                 "traffic": pv.get("hbm_bytes_per_launch"),
                 "traffic_note": ("HBM bytes per launch from rocprofv3 FETCH_SIZE*2 + WRITE_SIZE (profiles/%s, "
-                                 "same kernel build, separate --pmc passes); algorithmic input is 608 B/verify, the "
-                                 "rest is the per-lane [j]A/[j]R tables (~15 KB/verify) and spills" % PMC_PROFILE)
+                                 "same kernel build, separate --pmc passes; the config-2 launch, grouped by grid size); "
+                                 "algorithmic bytes are ~15.6 KB/verify: 608 B of input, the lane-major per-lane "
+                                 "[j]A/[j]R tables (2,880 B written, ~10.5 KB read) and 13 comb lines of B "
+                                 "(1.7 KB)" % PMC_PROFILE)
                 if pv else None,
                 "kernel": "k_ed25519_verify<strict>", "kernel_ms": round(kernel_ms, 3),
                 "mads_per_verify": mads,
