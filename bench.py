@@ -286,11 +286,69 @@ def bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_r
         ok &= hashlib.sha512(b).digest()[:32] == out[i].cpu().numpy().tobytes()
     padded = (ml + 17 + 127) // 128 * 128
     gbs = m_total * ml / wall * steps / 1e9 if wall > 0 else 0.0
-    return {"value": round(gbs, 2), "unit": "GB/s (message bytes)", "workload": "cfg4: %d x %d B" % (m_total, ml),
-            "ms_per_step": round(wall * 1e3 / steps, 3), "kernel_ms": round(kms, 3),
-            "hbm_frac": round((m * padded / (kms * 1e-3)) / 1e9 / HBM_PEAK_GBS, 4),
-            "note": "k_sha512_pipe: per 64 messages a producer wave expands K+W into LDS, a consumer wave runs the rounds; bound by the consumer wave's serial per-block stream (latency-bound, SURVEY H2), not HBM",
-            "spot_check_ok": bool(ok)}
+    pv = (load_profile(PMC_PROFILE) or {}).get("kernels", {}).get("sha512", {})
+    res = {"value": round(gbs, 2), "unit": "GB/s (message bytes)", "workload": "cfg4: %d x %d B" % (m_total, ml),
+           "ms_per_step": round(wall * 1e3 / steps, 3), "kernel_ms": round(kms, 3),
+           "hbm_frac": round((m * padded / (kms * 1e-3)) / 1e9 / HBM_PEAK_GBS, 4),
+           "valu_issue_share": round(pv["valu_issue_share_4cyc"], 3) if "valu_issue_share_4cyc" in pv else None,
+           "note": "k_sha512_pipe: per 64 messages a producer wave expands K+W into LDS, a consumer wave runs the rounds; bound by the consumer wave's serial per-block stream (latency-bound, SURVEY H2), not HBM; valu_issue_share from the PMC profile (256 consumer + 256 producer waves on 1,024 SIMDs)",
+           "spot_check_ok": bool(ok)}
+    if world == 1 and not args.no_cpu:
+        res["cpu_baseline"] = sha_cpu_baseline(args, data, out, m, ml)
+    return res
+
+
+def sha_cpu_baseline(args, data, out, m, ml):
+    """Config 4 on the host cores: the oracle's C SHA-512 (oracle/ntoracle.c, FIPS 180-4
+    restatement of sha2's software compress) over a bounded sample of the same
+    messages, args.cpu_threads threads, median of 3 runs; digests compared with the GPU's."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle
+    orc = _oracle.load()
+    th = args.cpu_threads
+    k = int(min(m, max(th * 8, 1024)))             # 1,024 x 500 KB = 512 MB of host copy
+    host = data[:k * ml].cpu().numpy()
+    offs = np.arange(k, dtype=np.uint64) * ml
+    lens = np.full(k, ml, np.uint64)
+    t0 = time.perf_counter()
+    orc.sha512_trunc32_many(host, offs[:1], lens[:1], nthreads=1)
+    one = time.perf_counter() - t0
+    # repeat the sample until ~args.cpu_seconds of CPU work, in 3 timed runs (median)
+    reps = max(1, int(round(args.cpu_seconds / 3 / (k * one))))
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dig = orc.sha512_trunc32_many(host, offs, lens, nthreads=th)
+        times.append((time.perf_counter() - t0) / reps)
+    dt = sorted(times)[1]
+    gpu = out[:k].cpu().numpy()
+    agree = int((dig == gpu).all(axis=1).sum())
+    # external comparator: OpenSSL's SHA-512 through hashlib (releases the GIL), th Python threads
+    import hashlib
+    import threading
+    ext_dig = [None] * k
+
+    def work(t):
+        for i in range(t, k, th):
+            ext_dig[i] = hashlib.sha512(memoryview(host)[i * ml:(i + 1) * ml]).digest()[:32]
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ts = [threading.Thread(target=work, args=(t,)) for t in range(th)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    edt = (time.perf_counter() - t0) / reps
+    eagree = sum(int(ext_dig[i] == gpu[i].tobytes()) for i in range(k))
+    return {"value": round(k * ml / dt / 1e9, 3), "unit": "GB/s (message bytes)", "cores": th, "kind": "port",
+            "sample": "first %d of the same %d-B cfg4 messages (%.0f MB) hashed %d times per run, median of 3 "
+                      "runs (%.2f s wall each)" % (k, ml, k * ml / 1e6, reps, dt * reps),
+            "single_thread_gbs": round(ml / one / 1e9, 3),
+            "digests_agree_with_gpu": "%d/%d" % (agree, k),
+            "external": {"name": "OpenSSL SHA-512 via Python hashlib", "value": round(k * ml / edt / 1e9, 3),
+                         "unit": "GB/s (message bytes)", "cores": th, "kind": "external",
+                         "digests_agree_with_gpu": "%d/%d" % (eagree, k)}}
 
 
 def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_ranks):
