@@ -228,6 +228,8 @@ def main():
     # ---------------------------------------------------------------- config 4: SHA-512 GB/s
     if not args.no_sha:
         line["sha512"] = bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_ranks)
+        line["sha512"]["real_batch"] = bench_sha_real(args, torch, dev, be, sp, stream, world, rank, barrier,
+                                                      max_over_ranks)
 
     # ---------------------------------------------------------------- config 3: certificates
     if not args.no_certs:
@@ -296,6 +298,57 @@ def bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_r
     if world == 1 and not args.no_cpu:
         res["cpu_baseline"] = sha_cpu_baseline(args, data, out, m, ml)
     return res
+
+
+def bench_sha_real(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_ranks):
+    """SURVEY §8(d) config 4 variants on the REAL worker batch: the bincode
+    WorkerMessage::Batch of 977 x 512-B transactions (508,052 B, the digest
+    worker/src/processor.rs:38 computes; golden digest in
+    tests/golden/sha512_vectors.json).  One batch alone (the latency the
+    Processor sees per call) and 16,384 copies sharded over ranks."""
+    import hashlib
+    import struct
+    from ntcrypto import dist as nd
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _oracle import expand
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "sha512_vectors.json")))
+    rb = gold["reference_fixtures"]["real_batch_977x512"]
+    txs = [expand((rb["tx_label"] % i).encode(), rb["tx_len"]) for i in range(rb["ntx"])]
+    real = struct.pack("<IQ", 0, len(txs)) + b"".join(struct.pack("<Q", len(t)) + t for t in txs)
+    bl = len(real)
+    one = torch.frombuffer(bytearray(real), dtype=torch.uint8).to(dev)
+    m_total = args.sha_msgs
+    lo, hi = nd.shard(m_total, world, rank)
+    m = hi - lo
+    data = one.repeat(m)
+    off = torch.arange(m, dtype=torch.int64, device=dev) * bl
+    ln = torch.full((m,), bl, dtype=torch.int64, device=dev)
+    out = torch.empty((m, 32), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+
+    def timed(k, reps):
+        be.dev_sha512(0, sp, data.data_ptr(), off.data_ptr(), ln.data_ptr(), k, out.data_ptr())
+        barrier()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(reps):
+            be.dev_sha512(0, sp, data.data_ptr(), off.data_ptr(), ln.data_ptr(), k, out.data_ptr())
+        ev1.record(stream)
+        barrier()
+        return max_over_ranks(time.perf_counter() - t0) / reps, ev0.elapsed_time(ev1) / reps
+
+    single_wall, single_k = timed(1, 3)
+    ok1 = out[0].cpu().numpy().tobytes().hex() == rb["digest32"]
+    wall, kms = timed(m, max(1, min(args.steps, 3)))
+    d = out.cpu().numpy()
+    okall = bool((d == d[0]).all()) and d[0].tobytes().hex() == rb["digest32"]
+    return {"bytes": bl, "digest_matches_golden": bool(ok1 and okall),
+            "single_batch_ms": round(single_k, 3),
+            "single_batch_note": "one 508,052-B batch = one lane's serial chain of 3,970 blocks: the per-call "
+                                 "latency a lone Processor call would see (SURVEY H3; batching via DigestBatcher)",
+            "copies": m_total, "gbs": round(m_total * bl / wall / 1e9, 2), "kernel_ms": round(kms, 3)}
 
 
 def sha_cpu_baseline(args, data, out, m, ml):
