@@ -193,3 +193,25 @@ def test_sodium_comparator_matches_corpus(oracle):
     r = oracle.sodium_verify_many(lib, d["pk"], d["sig"], d["msg"], d["off"], d["len"], 4)
     assert r is not None
     assert np.array_equal(r.astype(bool), d["strict"].astype(bool))
+
+
+def test_bench_sha_cpu_baseline_checks_digests():
+    """bench.py's config-4 CPU leg (oracle C SHA-512 + hashlib comparator) reports
+    agreement against the digests it is handed -- and catches a wrong one."""
+    import sys
+    import types
+    import hashlib
+    import torch
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    m, ml = 8, 1000
+    data = torch.from_numpy(np.random.default_rng(2).integers(0, 256, m * ml, dtype=np.uint8))
+    dig = np.stack([np.frombuffer(hashlib.sha512(data[i * ml:(i + 1) * ml].numpy().tobytes()).digest()[:32],
+                                  np.uint8) for i in range(m)])
+    dig[5, 0] ^= 1
+    res = bench.sha_cpu_baseline(types.SimpleNamespace(cpu_threads=2, cpu_seconds=0.05), data,
+                                 torch.from_numpy(dig), m, ml)
+    assert res["digests_agree_with_gpu"] == "7/8"
+    assert res["external"]["digests_agree_with_gpu"] == "7/8"
+    assert res["value"] > 0 and res["cores"] == 2
