@@ -54,6 +54,11 @@ extern "C" {
 
 #define NT_MODE_STRICT 0       /* dalek verify_strict */
 #define NT_MODE_COFACTORLESS 1 /* per-entry rule of dalek verify_batch */
+/* Key-cache entry points only: per signature, bit 31 of key_idx set = strict
+ * (Header/Vote::verify), clear = cofactorless (Certificate::verify's votes), so a
+ * drained batch of headers, votes and certificate votes is one launch. */
+#define NT_MODE_MIXED 2
+#define NT_KEY_STRICT_BIT 0x80000000u
 
 typedef struct nt_ctx nt_ctx;
 

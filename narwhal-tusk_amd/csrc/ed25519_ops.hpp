@@ -424,6 +424,13 @@ NT_HD NT_INLINE void verify_n(uint32_t ok[N], const uint32_t* const A[N], const 
 
 // Key-cache variant.  meta = the key's kKey* bits.
 enum : uint32_t { kKeyDecodes = 1u, kKeySmallOrder = 2u };
+// set by the kMixed loader in the meta it hands over: this signature is checked strictly
+constexpr uint32_t kKeyWantStrict = 0x80000000u;
+// strictness of one signature: the mode, or in kMixed mode the loader's per-signature bit
+template <int MODE>
+NT_HD NT_INLINE bool is_strict(uint32_t meta) {
+  return MODE == kStrict || (MODE == kMixed && (meta & kKeyWantStrict));
+}
 
 // One cached verification up to R' = [s]B - [k]A (extended), no decompression
 // of A and no doublings: 16 + 16 wide-comb additions.  Returns the s / key flags.
@@ -432,7 +439,7 @@ NT_HD NT_INLINE uint32_t cached_point(ge_p3& acc, uint32_t meta, const uint32_t 
                                       const uint32_t Sw[8], const uint8_t* msg, uint64_t len, const WCombA& ca,
                                       const WCombB& cb) {
   uint32_t okj = sc_is_canonical(Sw) & (meta & kKeyDecodes ? 1u : 0u);
-  if (MODE == kStrict) okj &= (meta & kKeySmallOrder) ? 0u : 1u;
+  if (is_strict<MODE>(meta)) okj &= (meta & kKeySmallOrder) ? 0u : 1u;
   uint32_t k[8];
   hram_scalar(k, Rw, Aw, msg, len);
   ge_p3_0(acc);
@@ -444,14 +451,14 @@ NT_HD NT_INLINE uint32_t cached_point(ge_p3& acc, uint32_t meta, const uint32_t 
 // Compare of one projective R' with the encoding Rw given zi = Z^-1 (see
 // finish_compare); strict mode adds the small-order test on R'.
 template <int MODE>
-NT_HD NT_INLINE uint32_t compare_one(const ge_p2& P, const fe& zi, const uint32_t Rw[8]) {
+NT_HD NT_INLINE uint32_t compare_one(const ge_p2& P, const fe& zi, const uint32_t Rw[8], bool strict) {
   fe x, y;
   fe_mul(x, P.X, zi);
   fe_mul(y, P.Y, zi);
   uint32_t yw[8];
   fe_tobytes_w(yw, y);
   uint32_t r = enc_matches(x, yw, Rw);
-  if (MODE == kStrict) r &= torsion_y_words(yw) ^ 1u;  // R' on the curve: small order <=> torsion y
+  if (strict) r &= torsion_y_words(yw) ^ 1u;  // R' on the curve: small order <=> torsion y
   return r;
 }
 
@@ -463,7 +470,7 @@ NT_HD NT_INLINE uint32_t compare_one(const ge_p2& P, const fe& zi, const uint32_
 // lane independent of N (the kernel's stash lives in global memory).
 template <int MODE, int N, class Loader, class WCombB, class Stash>
 NT_HD NT_INLINE uint32_t verify_cached_batch(const Loader& ld, const WCombB& cb, Stash& st) {
-  uint32_t okbits = 0;
+  uint32_t okbits = 0, strictbits = 0;
   fe acc;
 #pragma unroll 1
   for (int j = 0; j < N; ++j) {
@@ -474,6 +481,7 @@ NT_HD NT_INLINE uint32_t verify_cached_batch(const Loader& ld, const WCombB& cb,
     ld.get(j, meta, Aw, Rw, Sw, msg, len, ca);
     ge_p3 P;
     okbits |= cached_point<MODE>(P, meta, Aw, Rw, Sw, msg, len, ca, cb) << j;
+    strictbits |= (is_strict<MODE>(meta) ? 1u : 0u) << j;
     if (j == 0) acc = P.Z;
     else fe_mul(acc, acc, P.Z);
     ge_p2 P2;
@@ -497,7 +505,7 @@ NT_HD NT_INLINE uint32_t verify_cached_batch(const Loader& ld, const WCombB& cb,
     }
     uint32_t Rw[8];
     ld.rbytes(j, Rw);
-    okbits &= ~((compare_one<MODE>(P, zi, Rw) ^ 1u) << j);
+    okbits &= ~((compare_one<MODE>(P, zi, Rw, (strictbits >> j) & 1u) ^ 1u) << j);
   }
   return okbits;
 }

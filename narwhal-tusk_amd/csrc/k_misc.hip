@@ -394,11 +394,13 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
       d_combB, d_stash, d_out_words + lo / 64, s
     hipError_t e;
     if (key_bits == kKeyCombWide)
-      e = mode == kStrict ? launch_keyset_m<kStrict, kKeyCombWide>(NT_KS_ARGS)
-                          : launch_keyset_m<kCofactorless, kKeyCombWide>(NT_KS_ARGS);
+      e = mode == kStrict   ? launch_keyset_m<kStrict, kKeyCombWide>(NT_KS_ARGS)
+          : mode == kMixed  ? launch_keyset_m<kMixed, kKeyCombWide>(NT_KS_ARGS)
+                            : launch_keyset_m<kCofactorless, kKeyCombWide>(NT_KS_ARGS);
     else if (key_bits == kKeyCombNarrow)
-      e = mode == kStrict ? launch_keyset_m<kStrict, kKeyCombNarrow>(NT_KS_ARGS)
-                          : launch_keyset_m<kCofactorless, kKeyCombNarrow>(NT_KS_ARGS);
+      e = mode == kStrict   ? launch_keyset_m<kStrict, kKeyCombNarrow>(NT_KS_ARGS)
+          : mode == kMixed  ? launch_keyset_m<kMixed, kKeyCombNarrow>(NT_KS_ARGS)
+                            : launch_keyset_m<kCofactorless, kKeyCombNarrow>(NT_KS_ARGS);
     else
       e = hipErrorInvalidValue;
 #undef NT_KS_ARGS

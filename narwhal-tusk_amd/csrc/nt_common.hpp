@@ -27,6 +27,7 @@ namespace nt {
 enum VerifyMode : int {
   kStrict = 0,        // dalek verify_strict (crypto/src/lib.rs:200-204)
   kCofactorless = 1,  // per-entry rule of dalek verify_batch, SURVEY.md A.3
+  kMixed = 2,         // key-cache only: per signature, key_idx bit 31 set = strict, clear = cofactorless
 };
 
 // Digit widths of the committee-key combs (ed25519_ops.hpp, wide combs)

@@ -949,7 +949,8 @@ int nt_keyset_info(const nt_keyset* ks, uint32_t* comb_bits, uint64_t* bytes_per
 int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const uint32_t* key_idx,
                              const uint8_t* sig64, const uint8_t* msg, const uint64_t* off,
                              const uint64_t* len, uint64_t n, uint8_t* out_bitmap) {
-  if (!ctx || !ks || ks->ctx != ctx || (mode != NT_MODE_STRICT && mode != NT_MODE_COFACTORLESS)) return NT_EINVAL;
+  if (!ctx || !ks || ks->ctx != ctx || (mode != NT_MODE_STRICT && mode != NT_MODE_COFACTORLESS && mode != NT_MODE_MIXED))
+    return NT_EINVAL;
   if (n && (!key_idx || !sig64 || !off || !len || !out_bitmap)) return NT_EINVAL;
   if (n == 0) return NT_OK;
   return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
@@ -1040,7 +1041,8 @@ int nt_dev_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int dev, void
                                  const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
                                  uint64_t* d_out_words) {
   Device* dv = dev_of(ctx, dev);
-  if (!dv || !ks || ks->ctx != ctx || (mode != NT_MODE_STRICT && mode != NT_MODE_COFACTORLESS)) return NT_EINVAL;
+  if (!dv || !ks || ks->ctx != ctx || (mode != NT_MODE_STRICT && mode != NT_MODE_COFACTORLESS && mode != NT_MODE_MIXED))
+    return NT_EINVAL;
   NT_TRY(hipSetDevice(dv->ordinal));
   hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
   const auto& pd = ks->dev[dev];

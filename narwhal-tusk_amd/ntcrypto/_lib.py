@@ -14,6 +14,8 @@ LIB_PATH = os.environ.get("NTCRYPTO_LIB", os.path.join(PKG_ROOT, "lib", "libntcr
 
 NT_MODE_STRICT = 0
 NT_MODE_COFACTORLESS = 1
+NT_MODE_MIXED = 2             # key-cache only: key_idx bit 31 = strict
+NT_KEY_STRICT_BIT = 0x80000000
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)

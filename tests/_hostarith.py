@@ -87,10 +87,13 @@ def verify_trivial(mode, pk, sig, msg):
     return bool(load().nth_verify_trivial(mode, pk, sig, msg, ctypes.c_uint64(len(msg))))
 
 
-def verify_cached4(mode, entries):
+def verify_cached4(mode, entries, strict_mask=0):
     """Four (pk, sig, msg) through the key-cache kernel's path: 4 signatures per
-    lane, one inversion (verify_cached_batch<.., 4>)."""
+    lane, one inversion (verify_cached_batch<.., 4>).  mode 2 = mixed: entry j
+    is checked strictly iff bit j of strict_mask (the kernel's key_idx bit 31)."""
     assert len(entries) == 4
+    if mode == 2:
+        mode = 2 | (strict_mask << 8)
     out = (ctypes.c_int * 4)()
     msgs = [e[2] for e in entries]
     mp = (ctypes.c_char_p * 4)(*msgs)

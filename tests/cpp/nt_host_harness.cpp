@@ -283,7 +283,11 @@ int nth_verify_cached_n(int mode, int nsig, const uint8_t* pk, const uint8_t* si
   HostLoader ld{A, S, msgs, lens, meta, ca};
   HostStash st;
   uint32_t bits;
-  if (nsig == 2) bits = mode == 0 ? verify_cached_batch<kStrict, 2>(ld, bcomb(), st)
+  if ((mode & 0xff) == kMixed) {  // mode = kMixed | strict_mask << 8 (the kernel's key_idx bit 31)
+    for (int j = 0; j < nsig; ++j)
+      if ((mode >> (8 + j)) & 1) meta[j] |= kKeyWantStrict;
+    bits = nsig == 2 ? verify_cached_batch<kMixed, 2>(ld, bcomb(), st) : verify_cached_batch<kMixed, 4>(ld, bcomb(), st);
+  } else if (nsig == 2) bits = mode == 0 ? verify_cached_batch<kStrict, 2>(ld, bcomb(), st)
                                   : verify_cached_batch<kCofactorless, 2>(ld, bcomb(), st);
   else bits = mode == 0 ? verify_cached_batch<kStrict, 4>(ld, bcomb(), st)
                         : verify_cached_batch<kCofactorless, 4>(ld, bcomb(), st);

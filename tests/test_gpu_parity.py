@@ -225,6 +225,8 @@ def test_keyset_corpus(be, corpus, bits, monkeypatch):
     n = len(corpus["pk"])
     got_s = np.zeros(n, bool)
     got_c = np.zeros(n, bool)
+    got_m = np.zeros(n, bool)
+    want_strict = (np.arange(n) % 3) == 1      # NT_MODE_MIXED: these entries strict, the rest cofactorless
     for k0 in range(0, len(uniq), per_set):
         ks = be.keyset(uniq[k0:k0 + per_set])
         assert ks.info()[0] == bits
@@ -233,11 +235,16 @@ def test_keyset_corpus(be, corpus, bits, monkeypatch):
         args = (corpus["sig"][sel], corpus["msg"], corpus["off"][sel], corpus["len"][sel])
         got_s[sel] = ks.verify(ntcrypto.NT_MODE_STRICT, idx, *args)
         got_c[sel] = ks.verify(ntcrypto.NT_MODE_COFACTORLESS, idx, *args)
+        midx = idx | np.where(want_strict[sel], np.uint32(ntcrypto.NT_KEY_STRICT_BIT), np.uint32(0))
+        got_m[sel] = ks.verify(ntcrypto.NT_MODE_MIXED, midx.astype(np.uint32), *args)
+        # outside mixed mode bit 31 is just an unknown key index -> reject
+        assert not ks.verify(ntcrypto.NT_MODE_STRICT, midx.astype(np.uint32) | np.uint32(1 << 31), *args).any()
         # unknown key index -> reject
         assert not ks.verify(ntcrypto.NT_MODE_STRICT, np.full(len(sel), per_set + 5, np.uint32), *args).any()
         ks.close()
     assert np.array_equal(got_s, corpus["strict"].astype(bool))
     assert np.array_equal(got_c, corpus["batch_rule"].astype(bool))
+    assert np.array_equal(got_m, np.where(want_strict, corpus["strict"], corpus["batch_rule"]).astype(bool))
 
 
 def test_keyset_comb_width_choice(be):

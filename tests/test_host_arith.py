@@ -150,6 +150,10 @@ def test_corpus_quads_through_keyset_path():
         for mode, key in ((0, "strict"), (1, "batch_rule")):
             want = tuple(bool(d[key][j]) for j in idx)
             assert H.verify_cached4(mode, [entry(j) for j in idx]) == want, (i, mode)
+        # mixed mode (one launch for header + vote signatures): per-entry strictness
+        mask = (i // 4) % 16
+        want = tuple(bool(d["strict" if (mask >> k) & 1 else "batch_rule"][j]) for k, j in enumerate(idx))
+        assert H.verify_cached4(2, [entry(j) for j in idx], strict_mask=mask) == want, (i, "mixed", mask)
 
 
 def test_sc_halfsize_properties():

@@ -11,7 +11,7 @@ mkdir -p "$OUT/obj"
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $EXTRA"
 pids=()
 for tu in k_misc k_verify_strict k_verify_cofactorless k_keyset_strict_w20 k_keyset_strict_w16 \
-          k_keyset_cofactorless_w20 k_keyset_cofactorless_w16; do
+          k_keyset_cofactorless_w20 k_keyset_cofactorless_w16 k_keyset_mixed_w20 k_keyset_mixed_w16; do
   /opt/rocm/bin/hipcc $FLAGS -c -x hip "$SRC/$tu.hip" -o "$OUT/obj/$tu.o" & pids+=($!)
 done
 /opt/rocm/bin/hipcc $FLAGS -c -x hip "$SRC/ntcrypto.cpp" -o "$OUT/obj/ntcrypto.o" & pids+=($!)
