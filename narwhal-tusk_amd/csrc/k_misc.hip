@@ -203,13 +203,17 @@ __global__ void k_wcomb_fill(const uint32_t* __restrict__ bases, uint32_t nkeys,
 // Per-signature message slices of certificate groups (message g = 32 bytes at
 // 32 g): the host entry points send first/cnt per group instead of 16 bytes of
 // offset/length per signature over PCIe.
+// One wave per group: the lanes write the group's consecutive entries, so
+// the stores of a wave are contiguous (a thread per group strided them by
+// cnt x 8 bytes: one cache line per lane per store).
 __global__ __launch_bounds__(kBlock) void k_group_msgs(const uint64_t* __restrict__ first,
                                                       const uint32_t* __restrict__ cnt, uint64_t G,
                                                       uint64_t* __restrict__ off, uint64_t* __restrict__ len) {
-  const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t g = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63u;
   if (g >= G) return;
   const uint64_t f = first[g], c = cnt[g];
-  for (uint64_t q = 0; q < c; ++q) {
+  for (uint64_t q = lane; q < c; q += 64) {
     off[f + q] = 32 * g;
     len[f + q] = 32;
   }
@@ -326,7 +330,8 @@ hipError_t launch_group_and(const uint64_t* d_first, const uint32_t* d_cnt, uint
 hipError_t launch_group_msgs(const uint64_t* d_first, const uint32_t* d_cnt, uint64_t G, uint64_t* d_off,
                              uint64_t* d_len, hipStream_t s) {
   if (G == 0) return hipSuccess;
-  const uint64_t blocks = (G + kBlock - 1) / kBlock;
+  const uint64_t groups_per_block = kBlock / 64;
+  const uint64_t blocks = (G + groups_per_block - 1) / groups_per_block;
   hipLaunchKernelGGL(k_group_msgs, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_first, d_cnt, G, d_off, d_len);
   return hipGetLastError();
 }
