@@ -23,13 +23,18 @@ curve25519-dalek u64 backend) on a bounded sample of the same workload,
 rank 0 at N=1 only -- a reported baseline, also used as an in-bench parity
 check of the sample.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under
-torch.distributed.run (one process per GPU; gloo only for the barrier and the
-max-over-ranks timing -- the data path has no collective).
+Launch: python bench.py [--gpus N --steps K --warmup W].  One process per GPU;
+gloo only for the barrier and the max-over-ranks timing (the data path has no
+collective).  Under torch.distributed.run (WORLD_SIZE set) each process is one
+rank; a plain `python bench.py --gpus N` with N > 1 starts the N ranks itself
+(torch.distributed.run as a child process, before this process touches the
+GPU) and exits with their status.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -67,8 +72,40 @@ def parse():
     return ap.parse_args()
 
 
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_launch(argv, n, port, env=None):
+    """(argv, env) of the child that runs `n` ranks of this script: one process
+    per GPU through torch.distributed.run on 127.0.0.1 (the path
+    shards by index, each rank verifies its own shard).  Every rank gets
+    LOCAL_RANK = its device ordinal from the launcher."""
+    env = dict(os.environ if env is None else env)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return cmd, env
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # nothing here has initialised the GPU: start the ranks as a child and
+        # report its status (no exec from this process)
+        cmd, env = rank_launch(sys.argv[1:], args.gpus, free_port())
+        sys.exit(subprocess.run(cmd, env=env).returncode)
+    if os.environ.get("NT_BENCH_RANK_PROBE"):
+        # launcher rehearsal (tests/test_bench_launch.py): report the rank layout, touch no GPU
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": int(os.environ.get("WORLD_SIZE", "1")),
+                          "local_rank": local, "device": int(os.environ.get("NT_BENCH_DEVICE", local))}), flush=True)
+        return
     import torch
     import torch.distributed as dist
 
@@ -309,8 +346,6 @@ def bench_sha_real(args, torch, dev, be, sp, stream, world, rank, barrier, max_o
     import hashlib
     import struct
     from ntcrypto import dist as nd
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from _oracle import expand
     gold = json.load(open(os.path.join(ROOT, "tests", "golden", "sha512_vectors.json")))
     rb = gold["reference_fixtures"]["real_batch_977x512"]
     txs = [expand((rb["tx_label"] % i).encode(), rb["tx_len"]) for i in range(rb["ntx"])]
@@ -729,6 +764,19 @@ def sodium_baseline(orc, pk_h, sig_h, msg_h, L, got, th, seconds):
             "unit": "verifies/s", "cores": th, "kind": "external",
             "sample": "first %d of the same cfg2 verifies, median of 3 runs (%.1f s wall each)" % (sample, dt),
             "single_thread_us_per_verify": round(per * 1e6, 2), "verdicts_agree_with_gpu": "%d/%d" % (agree, sample)}
+
+
+def expand(label: bytes, n: int) -> bytes:
+    """Deterministic synthetic bytes (SHA-512 counter mode), the generator of
+    tests/golden/make_golden.py's real-batch fixture."""
+    import hashlib
+    import struct
+    out = bytearray()
+    i = 0
+    while len(out) < n:
+        out += hashlib.sha512(label + struct.pack("<Q", i)).digest()
+        i += 1
+    return bytes(out[:n])
 
 
 def mads_per_verify(msg_len):

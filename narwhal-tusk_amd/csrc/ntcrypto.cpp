@@ -1,8 +1,9 @@
 // ntcrypto.cpp -- host side of the C ABI (include/ntcrypto.h).
 //
-// Owns one `Device` per GPU: a non-blocking HIP stream, the wide comb of B
-// (67 MB), the per-lane [k]A table workspace and grow-only device/pinned
-// staging buffers.
+// Owns one `Device` per GPU (per entry of nt_init_devices: a repeated ordinal
+// gets its own): non-blocking HIP streams, the wide comb of B (20-bit digits,
+// 872 MB per Device; 67 MB in a -DNT_BCOMB_BITS=16 build), the per-lane [k]A
+// table workspace and grow-only device/pinned staging buffers.
 // Host entry points shard items over devices by contiguous index ranges (one
 // host thread per device), stage through pinned memory, launch, and gather the
 // bitmaps / digests.  There is deliberately no CPU compute path: if HIP or the
@@ -94,6 +95,7 @@ struct Device {
   uint32_t sign_blocks = 0;
   uint32_t cus = 0;
   hipEvent_t ws_done = nullptr;  // orders every kernel that uses d_ws, whatever its stream
+  hipEvent_t stash_done = nullptr;  // same for the key-cache stash d[B_STASH] (host and device API)
   // host entry points: chunk c's H2D copies go on cstream and chunk c's kernels
   // wait for cev[c] on `stream`, so copies of chunk c+1 overlap kernels of chunk c
   hipStream_t cstream = nullptr;
@@ -119,6 +121,7 @@ struct Device {
     if (d_combB) (void)hipFree(d_combB);
     if (d_ws) (void)hipFree(d_ws);
     if (ws_done) (void)hipEventDestroy(ws_done);
+    if (stash_done) (void)hipEventDestroy(stash_done);
     for (auto& e : cev)
       if (e) (void)hipEventDestroy(e);
     if (stream2) (void)hipStreamSynchronize(stream2);
@@ -139,6 +142,7 @@ struct Device {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NT_ENODEV;
     NT_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     NT_TRY(hipEventCreateWithFlags(&ws_done, hipEventDisableTiming));
+    NT_TRY(hipEventCreateWithFlags(&stash_done, hipEventDisableTiming));
     NT_TRY(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
     for (auto& e : cev) NT_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     NT_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
@@ -162,6 +166,7 @@ struct Device {
     cus = (uint32_t)prop.multiProcessorCount;
     if (hipMalloc(&d_ws, nt::ws_bytes_per_slot() * ws_slots) != hipSuccess) return NT_ENOMEM;
     NT_TRY(hipEventRecord(ws_done, stream));
+    NT_TRY(hipEventRecord(stash_done, stream));
     NT_TRY(hipStreamSynchronize(stream));
     return NT_OK;
   }
@@ -219,6 +224,18 @@ struct Device {
                           out, stream2) != hipSuccess ||
         hipEventRecord(ws2_done, stream2) != hipSuccess)
       return NT_EHIP;
+    return NT_OK;
+  }
+
+  // Key-cache launch on stream s with stash st: launches that use the shared
+  // d[B_STASH] (host chunks on `stream`, device-API calls on any stream) wait
+  // for its previous user and mark it, like d_ws; stash2 belongs to stream2.
+  template <class F>
+  int keyset_launch(hipStream_t s, void* st, F&& launch) {
+    const bool shared = st == d[B_STASH].p;
+    if (shared && hipStreamWaitEvent(s, stash_done, 0) != hipSuccess) return NT_EHIP;
+    if (launch() != hipSuccess) return NT_EHIP;
+    if (shared && hipEventRecord(stash_done, s) != hipSuccess) return NT_EHIP;
     return NT_OK;
   }
 
@@ -794,9 +811,11 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
                                      (uint64_t*)doff, (uint64_t*)dlen, s));
         if (ks) {
           const auto& pd = *(const nt_keyset::PerDev*)pd_meta;
-          NT_TRY(nt::launch_verify_keyset(NT_MODE_COFACTORLESS, ks->bits, (const uint32_t*)dk, dsig, dmsg, doff, dlen, mc,
-                                          pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB,
-                                          (c & 1) ? dv.stash2.p : dv.d[B_STASH].p, dout, s));
+          void* st = (c & 1) ? dv.stash2.p : dv.d[B_STASH].p;
+          NT_CHK(dv.keyset_launch(s, st, [&] {
+            return nt::launch_verify_keyset(NT_MODE_COFACTORLESS, ks->bits, (const uint32_t*)dk, dsig, dmsg, doff, dlen,
+                                            mc, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, st, dout, s);
+          }));
         } else {
           NT_CHK(dv.verify_chunk((int)c, NT_MODE_COFACTORLESS, dk, dsig, dmsg, doff, dlen, mc, dout));
         }
@@ -975,11 +994,15 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
       NT_TRY(hipMemcpyAsync(dv.d[B_SIG].as<uint8_t>() + 64 * a, sig64 + 64 * (lo + a), (b - a) * 64,
                             hipMemcpyHostToDevice, dv.cstream));
       NT_TRY(dv.fence((int)c));
-      NT_TRY(nt::launch_verify_keyset(mode, ks->bits, dv.d[B_PK].as<uint32_t>() + a, dv.d[B_SIG].as<uint8_t>() + 64 * a,
-                                      dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>() + a,
-                                      dv.d[B_LEN].as<uint64_t>() + a, b - a, pd.d_meta, pd.d_enc, pd.d_comb,
-                                      ks->nkeys, dv.d_combB, (c & 1) ? dv.stash2.p : dv.d[B_STASH].p,
-                                      dv.d[B_OUT].as<uint64_t>() + a / 64, dv.cstr((int)c)));
+      void* st = (c & 1) ? dv.stash2.p : dv.d[B_STASH].p;
+      hipStream_t s = dv.cstr((int)c);
+      NT_CHK(dv.keyset_launch(s, st, [&] {
+        return nt::launch_verify_keyset(mode, ks->bits, dv.d[B_PK].as<uint32_t>() + a,
+                                        dv.d[B_SIG].as<uint8_t>() + 64 * a, dv.d[B_DATA].as<uint8_t>(),
+                                        dv.d[B_OFF].as<uint64_t>() + a, dv.d[B_LEN].as<uint64_t>() + a, b - a,
+                                        pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, st,
+                                        dv.d[B_OUT].as<uint64_t>() + a / 64, s);
+      }));
     }
     NT_TRY(dv.join());
     NT_TRY(hipMemcpyAsync(dv.h[B_OUT].p, dv.d[B_OUT].p, words * 8, hipMemcpyDeviceToHost, dv.stream));
@@ -1046,17 +1069,15 @@ int nt_dev_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int dev, void
   NT_TRY(hipSetDevice(dv->ordinal));
   hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
   const auto& pd = ks->dev[dev];
-  // the device's stash: device-API key-cache launches on one device must be
-  // ordered on one stream (they share it)
-  void* stash;
-  {
-    std::lock_guard<std::mutex> lk(dv->mu);
-    NT_CHK(dv->d[B_STASH].ensure(nt::keyset_stash_bytes(n)));
-    stash = dv->d[B_STASH].p;
-  }
-  NT_TRY(nt::launch_verify_keyset(mode, ks->bits, d_key_idx, d_sig64, d_msg, d_off, d_len, n, pd.d_meta, pd.d_enc, pd.d_comb,
-                                  ks->nkeys, dv->d_combB, stash, d_out_words, s));
-  return NT_OK;
+  // the device's stash, shared with the host entry points: ordered against
+  // every other user by stash_done, whatever the streams
+  std::lock_guard<std::mutex> lk(dv->mu);
+  NT_CHK(dv->d[B_STASH].ensure(nt::keyset_stash_bytes(n)));
+  void* stash = dv->d[B_STASH].p;
+  return dv->keyset_launch(s, stash, [&] {
+    return nt::launch_verify_keyset(mode, ks->bits, d_key_idx, d_sig64, d_msg, d_off, d_len, n, pd.d_meta, pd.d_enc,
+                                    pd.d_comb, ks->nkeys, dv->d_combB, stash, d_out_words, s);
+  });
 }
 
 int nt_dev_ed25519_sign(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_seed32,

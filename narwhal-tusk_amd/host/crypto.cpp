@@ -59,6 +59,8 @@ std::vector<uint8_t> base64_decode(const std::string& s) {
         if (v[j] < 0) throw std::invalid_argument("InvalidByte");
       }
     }
+    // base64 0.13 rejects non-zero unused bits in the last data symbol (InvalidLastSymbol)
+    if ((pad == 1 && (v[2] & 3)) || (pad == 2 && (v[1] & 15))) throw std::invalid_argument("InvalidLastSymbol");
     const uint32_t w = ((uint32_t)v[0] << 18) | ((uint32_t)v[1] << 12) | ((uint32_t)v[2] << 6) | (uint32_t)v[3];
     out.push_back((uint8_t)(w >> 16));
     if (pad < 2) out.push_back((uint8_t)(w >> 8));

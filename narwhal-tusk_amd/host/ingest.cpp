@@ -500,7 +500,14 @@ std::vector<DagError> Core::ingest_soa(const uint8_t* data, const uint64_t* off,
             weight += ki.stake[k];
           }
           if (e == DagError::Ok && weight < quorum) e = DagError::CertificateRequiresQuorum;
-          if (e != DagError::Ok) { res[i] = e; continue; }
+          if (e != DagError::Ok) {
+            // Header::verify (signature included) precedes the quorum loop
+            // (messages.rs:194-211): the header signature still goes to the strict
+            // launch, whose failure overrides this error below
+            res[i] = e;
+            add_sig(i, r.author, r.sig, r.id.data());
+            continue;
+          }
           o.gwho.push_back(i);
           o.first.push_back(dense);
           o.cnt.push_back((uint32_t)r.vote_cnt);

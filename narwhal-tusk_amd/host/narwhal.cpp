@@ -298,8 +298,11 @@ std::vector<DagError> Core::sanitize_batch(const std::vector<PrimaryMessage>& ms
       sk.push_back(h.author);
       ss.push_back(h.signature);
       if (need[i] == kCert) {
+        // Certificate::verify runs Header::verify -- signature included -- before
+        // the quorum loop (messages.rs:194-211): a failed quorum is reported only
+        // if the header signature passes, so the header stays in the strict launch
         const DagError q = quorum_check(m.certificate, cm);
-        if (q != DagError::Ok) { res[i] = q; s_of[i] = SIZE_MAX; continue; }
+        if (q != DagError::Ok) { res[i] = q; continue; }
         g_of[i] = gd.size();
         gd.push_back(dig[pre_at[i] + 1]);
         groups.push_back(&m.certificate.votes);
@@ -313,8 +316,9 @@ std::vector<DagError> Core::sanitize_batch(const std::vector<PrimaryMessage>& ms
     }
   }
   // 3) launch 2 (every header/vote signature) and launch 3 (every certificate's votes).
-  // A certificate whose header signature fails reports InvalidSignature either way,
-  // so its vote group may be checked in the same pass.
+  // A certificate whose header signature fails reports InvalidSignature whatever
+  // its quorum or votes, so its vote group may be checked in the same pass; one
+  // that failed the quorum check keeps that error unless its header signature fails.
   const auto sv = cache ? cache->verify_many(sd, sk, ss) : crypto::verify_many(sd, sk, ss);
   const auto gv = groups.empty() ? std::vector<bool>{}
                   : cache ? cache->verify_batch_many(gd, groups) : crypto::verify_batch_many(gd, groups);

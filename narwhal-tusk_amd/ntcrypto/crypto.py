@@ -60,6 +60,31 @@ class Digest:
         return base64.b64encode(self._b).decode()[:16]
 
 
+def b64decode_strict(s: str) -> bytes:
+    """base64 0.13 STANDARD decode as the reference's serde path uses it
+    (crypto/src/lib.rs:94-112, 152-160): standard alphabet, length a multiple of
+    4, '=' only as the last one or two symbols, and no non-zero unused bits in
+    the last data symbol (InvalidLastSymbol) -- the same rules as the C++
+    mirror's crypto::base64_decode.  Raises ValueError."""
+    if isinstance(s, str):
+        try:
+            s = s.encode("ascii")
+        except UnicodeEncodeError:
+            raise ValueError("InvalidByte") from None
+    if len(s) % 4:
+        raise ValueError("InvalidLength")
+    try:
+        b = base64.b64decode(s, validate=True)
+    except Exception:
+        raise ValueError("InvalidByte") from None
+    pad = len(s) - len(s.rstrip(b"="))
+    if pad:
+        last = base64.b64decode(s[-4:-pad] + b"A" * pad, validate=True)  # the unused bits land in the tail bytes
+        if last[-pad:] != bytes(pad):
+            raise ValueError("InvalidLastSymbol")
+    return b
+
+
 def sha512_digest(data: bytes) -> Digest:
     """Digest(Sha512::digest(data)[..32]) on the GPU (worker/src/processor.rs:38)."""
     return Digest(default_backend().digest_many([bytes(data)])[0].tobytes())
@@ -87,7 +112,7 @@ class PublicKey:
 
     @classmethod
     def decode_base64(cls, s: str) -> "PublicKey":
-        b = base64.b64decode(s)
+        b = b64decode_strict(s)
         if len(b) < 32:
             raise ValueError("InvalidLength")
         return cls(b[:32])
@@ -122,7 +147,7 @@ class SecretKey:
 
     @classmethod
     def decode_base64(cls, s: str) -> "SecretKey":
-        b = base64.b64decode(s)
+        b = b64decode_strict(s)
         if len(b) < 64:
             raise ValueError("InvalidLength")
         return cls(b[:64])
@@ -162,6 +187,18 @@ class Signature:
 
     @classmethod
     def new(cls, digest: Digest, secret: SecretKey) -> "Signature":
+        """crypto/src/lib.rs:185-191 (dalek Keypair::sign over the 32-byte digest).
+
+        TEST / CORPUS USE ONLY: this runs the library's batch signer
+        (nt_ed25519_sign_batch), which is NOT constant time, with the secret
+        key in device memory.  The product binding leaves
+        Signature::new / SignatureService on the reference's CPU path
+        (SURVEY §3.4); nothing in the hot path signs.
+        Deliberate divergence for malformed secrets: dalek's Keypair::from_bytes
+        only checks that the public half decompresses and then signs with those
+        bytes in H(R || A || M) (an invalid signature when they do not belong to
+        the seed); here a public half that is not the seed's key raises
+        ValueError instead.  No reference fixture covers that case."""
         seed = np.frombuffer(secret.seed(), np.uint8).reshape(1, 32)
         m = np.frombuffer(bytes(digest), np.uint8)
         pk, sig = default_backend().sign_batch(seed, m, np.array([0], np.uint64), np.array([32], np.uint64))
@@ -200,7 +237,9 @@ class Signature:
 
 
 class SignatureService:
-    """crypto/src/lib.rs:222-249: holds the secret key; returns signatures over digests."""
+    """crypto/src/lib.rs:222-249: holds the secret key; returns signatures over
+    digests.  TEST / CORPUS USE ONLY (see Signature.new: non-constant-time GPU
+    signer); the product keeps the reference's CPU SignatureService."""
 
     def __init__(self, secret: SecretKey):
         self._q = queue.Queue(100)

@@ -165,7 +165,14 @@ def _scenario(orc, rng):
         cert(header(keys[2], 9), keys[:4] + [keys[1]]), cert(header(keys[2], 9), keys[:4] + [stranger]),
         cert(header(keys[2], 9), keys[:5], bad_vote=keys[3]), cert(header(keys[5], 10), keys[1:6]),
         ([_rb(rng, 32)], keys[1]),
+        # header signature AND quorum both bad: Header::verify runs first, so
+        # InvalidSignature (messages.rs:194 before :199-211), not the quorum error
+        cert(header(keys[2], 9, bad_sig=True), keys[:3]),
+        cert(header(keys[2], 9, bad_sig=True), keys[:4] + [keys[1]]),
+        cert(header(keys[2], 9, bad_sig=True), keys[:4] + [stranger]),
     ]
+    assert [W.model_sanitize(com, gc_round, cur, o, lambda d, pk, s: orc.verify_strict(pk, s, d), None)
+            for o in objs[-3:]] == [W.INVALID_SIGNATURE] * 3
     wires = [W.message(o) for o in objs] + [b"\x02\x00\x00\x00garbage", b""]
     # a valid header whose payload entries arrive in descending order (non-canonical
     # bytes: the decoder's BTreeMap sorts them, so the id still matches)
