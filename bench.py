@@ -68,8 +68,67 @@ def parse():
     ap.add_argument("--no-ingest", action="store_true")
     ap.add_argument("--ingest-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-seconds of baseline work")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0 = every CPU this process may use, see host_cpu)")
     return ap.parse_args()
+
+
+def host_cpu():
+    """The host the CPU baselines run on: the machine's CPU count and model, and
+    how many of those CPUs this process may actually use (affinity mask and
+    cgroup CPU quota).  On the GPU pool a one-GPU box is a share of a larger
+    machine (16 CPUs per GPU) whose nproc counts every CPU of the machine:
+    threads beyond the share only time-slice, so the baseline runs on the
+    usable CPUs and `full_host_estimate` scales its per-thread rate to nproc."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = nproc
+    quota = None
+    for path, conv in (("/sys/fs/cgroup/cpu.max", lambda t: None if t[0] == "max" else int(t[0]) / int(t[1])),
+                       ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            with open(path) as f:
+                txt = f.read().split()
+            if conv is not None:
+                quota = conv(txt)
+            else:
+                q = int(txt[0])
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    per = int(f.read().split()[0])
+                quota = None if q <= 0 else q / per
+            break
+        except Exception:
+            continue
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    policy_cap = None
+    if quota is None and usable > 16 and os.environ.get("GRAFT_REPO_ROOT"):
+        policy_cap = 16  # the pool's per-GPU CPU share when the box does not enforce one
+        usable = 16
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except Exception:
+        pass
+    return {"nproc": nproc, "affinity_cpus": aff, "cgroup_quota_cpus": quota, "usable_cpus": usable,
+            "policy_cap": policy_cap, "model": model}
+
+
+def cpu_threads(args):
+    return args.cpu_threads if args.cpu_threads > 0 else host_cpu()["usable_cpus"]
+
+
+def full_host(rate, threads, host):
+    """Per-thread rate x the machine's CPU count: what the same code would reach
+    on every core of the host (an extrapolation, labelled as such)."""
+    return {"value": round(rate / threads * host["nproc"], 1), "cores": host["nproc"],
+            "note": "measured rate / %d threads x nproc %d (linear in cores: independent items, no shared "
+                    "state); an estimate, not a measurement" % (threads, host["nproc"])}
 
 
 def free_port():
@@ -393,7 +452,7 @@ def sha_cpu_baseline(args, data, out, m, ml):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle
     orc = _oracle.load()
-    th = args.cpu_threads
+    th = cpu_threads(args)
     k = int(min(m, max(th * 8, 1024)))             # 1,024 x 500 KB = 512 MB of host copy
     host = data[:k * ml].cpu().numpy()
     offs = np.arange(k, dtype=np.uint64) * ml
@@ -429,9 +488,13 @@ def sha_cpu_baseline(args, data, out, m, ml):
             t.join()
     edt = (time.perf_counter() - t0) / reps
     eagree = sum(int(ext_dig[i] == gpu[i].tobytes()) for i in range(k))
-    return {"value": round(k * ml / dt / 1e9, 3), "unit": "GB/s (message bytes)", "cores": th, "kind": "port",
+    host = host_cpu()
+    gbs = k * ml / dt / 1e9
+    return {"value": round(gbs, 3), "unit": "GB/s (message bytes)", "cores": th, "kind": "port",
+            "label": "FIPS 180-4 C restatement of sha2 0.9's software compress (oracle/sha512_ref.c)",
             "sample": "first %d of the same %d-B cfg4 messages (%.0f MB) hashed %d times per run, median of 3 "
                       "runs (%.2f s wall each)" % (k, ml, k * ml / 1e6, reps, dt * reps),
+            "host": host, "full_host_estimate": full_host(gbs, th, host),
             "single_thread_gbs": round(ml / one / 1e9, 3),
             "digests_agree_with_gpu": "%d/%d" % (agree, k),
             "external": {"name": "OpenSSL SHA-512 via Python hashlib", "value": round(k * ml / edt / 1e9, 3),
@@ -588,6 +651,8 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                     "ms_per_step": round(wall * 1e3 / steps, 3), "gpu_ms_per_step": round(kms, 3),
                     "mismatches_vs_expected": mism}
     ks.close()
+    if world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cert_cpu_baseline(args, hdr, hlen, ids, tmp_pk, hsig, cpre, vpk, vsig, quorum, expect)
     return {"value": out["keyset"]["certs_per_s"], "unit": "certificates/s",
             "workload": "cfg3: %d certificates, committee n=%d, %d votes + 1 header signature each, "
                         "%d-byte header preimage" % (G_total, nk, quorum, hlen),
@@ -599,6 +664,51 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                           "launches": "per step: 2 SHA-512 (header ids, certificate digests), 1 NT_MODE_MIXED key-cache "
                                       "verify (67 votes cofactorless + the header signature strict), 1 group AND"},
             **out}
+
+
+def cert_cpu_baseline(args, hdr, hlen, ids, hpk, hsig, cpre, vpk, vsig, quorum, expect):
+    """Config 3 on the host cores: Certificate::verify (primary/src/messages.rs:189-215)
+    per certificate = SHA-512 of the header preimage (id check), verify_strict of
+    the header signature, SHA-512 of the certificate digest preimage and dalek's
+    verify_batch of the votes -- computed as dalek computes it (random z_i, one
+    Straus multiscalar multiplication; oracle ntor_certificates_verify_many) --
+    on a bounded sample of the same certificates, verdicts compared."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle
+    orc = _oracle.load()
+    th = cpu_threads(args)
+    G = hdr.shape[0]
+
+    def run(k, threads):
+        h = hdr[:k].cpu().numpy()
+        first = np.arange(k, dtype=np.uint64) * quorum
+        t0 = time.perf_counter()
+        r = orc.certificates_verify_many(h.reshape(-1), np.arange(k, dtype=np.uint64) * hlen,
+                                         np.full(k, hlen, np.uint64), ids[:k].cpu().numpy(), hpk[:k].cpu().numpy(),
+                                         hsig[:k].cpu().numpy(), cpre[:k].cpu().numpy(),
+                                         vpk[:k * quorum].cpu().numpy(), vsig[:k * quorum].cpu().numpy(), first,
+                                         np.full(k, quorum, np.uint32), nthreads=threads)
+        return r, time.perf_counter() - t0
+
+    _, one = run(4, 1)
+    per = one / 4
+    sample = int(min(G, max(th * 8, args.cpu_seconds / per)))
+    times = []
+    for _ in range(3):
+        res, dt = run(sample, th)
+        times.append(dt)
+    dt = sorted(times)[1]
+    agree = int((res.astype(bool) == expect[:sample]).sum())
+    host = host_cpu()
+    return {"value": round(sample / dt, 1), "unit": "certificates/s", "cores": th, "kind": "port",
+            "label": "dalek-equivalent CPU restatement: Certificate::verify's 2 SHA-512 digests, verify_strict of "
+                     "the header and dalek's randomized verify_batch of the %d votes (Straus / NAF-5 multiscalar)"
+                     % quorum,
+            "sample": "first %d of the same cfg3 certificates, median of 3 runs (%.2f s wall each on %d threads)"
+                      % (sample, dt, th),
+            "single_thread_ms_per_certificate": round(per * 1e3, 3),
+            "host": host, "full_host_estimate": full_host(sample / dt, th, host),
+            "verdicts_agree_with_expected": "%d/%d" % (agree, sample)}
 
 
 def bench_ingest(args, be, world, rank, local, max_over_ranks, barrier):
@@ -707,7 +817,7 @@ def cpu_baseline(args, pk_h, sig_h, msg_h, L, got):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle
     orc = _oracle.load()
-    th = args.cpu_threads
+    th = cpu_threads(args)
     # calibrate: per-verify cost on one thread
     k = 256
     offs = (np.arange(k, dtype=np.uint64) * L)
@@ -725,9 +835,12 @@ def cpu_baseline(args, pk_h, sig_h, msg_h, L, got):
         times.append(time.perf_counter() - t0)
     dt = sorted(times)[1]
     agree = int((res.astype(bool) == got[:sample]).sum())
+    host = host_cpu()
     out = {"value": round(sample / dt, 1), "unit": "verifies/s", "cores": th, "kind": "port",
+           "label": "dalek-equivalent CPU restatement (oracle/: curve25519-dalek u64-backend field arithmetic -- radix 2^51, dedicated square, lazy add -- and dalek's verify algorithms)",
            "sample": "first %d of the same 1M cfg2 verifies, median of 3 runs (%.1f s wall each on %d threads)"
                      % (sample, dt, th),
+           "host": host, "full_host_estimate": full_host(sample / dt, th, host),
            "single_thread_us_per_verify": round(per * 1e6, 2),
            "verdicts_agree_with_gpu": "%d/%d" % (agree, sample)}
     ext = sodium_baseline(orc, pk_h, sig_h, msg_h, L, got, th, args.cpu_seconds)

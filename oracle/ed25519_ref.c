@@ -48,17 +48,31 @@ static void fe_carry(fe *h) {
   }
 }
 
-static void fe_add(fe *h, const fe *f, const fe *g) {
-  for (int i = 0; i < 5; ++i) h->v[i] = f->v[i] + g->v[i];
-  fe_carry(h);
+/* One weak reduction pass (curve25519-dalek FieldElement51::reduce): every
+ * carry is taken from the input limbs, then added once; limbs < 2^52 after. */
+static void fe_reduce(fe *h) {
+  const uint64_t c0 = h->v[0] >> 51, c1 = h->v[1] >> 51, c2 = h->v[2] >> 51, c3 = h->v[3] >> 51,
+                 c4 = h->v[4] >> 51;
+  h->v[0] = (h->v[0] & MASK51) + 19 * c4;
+  h->v[1] = (h->v[1] & MASK51) + c0;
+  h->v[2] = (h->v[2] & MASK51) + c1;
+  h->v[3] = (h->v[3] & MASK51) + c2;
+  h->v[4] = (h->v[4] & MASK51) + c3;
 }
 
-/* h = f - g; inputs carried (limbs < 2^52). Adds 8p to stay non-negative. */
+/* Lazy addition as in dalek (no reduction): inputs are mul/sq/sub outputs
+ * (limbs < 2^52) or sums of two of them; every consumer (mul/sq: limbs < 2^54,
+ * sub: g < 16p limbwise, tobytes: two carry passes) accepts limbs < 2^54. */
+static void fe_add(fe *h, const fe *f, const fe *g) {
+  for (int i = 0; i < 5; ++i) h->v[i] = f->v[i] + g->v[i];
+}
+
+/* h = f + 16p - g, one weak reduction (dalek Sub for FieldElement51). */
 static void fe_sub(fe *h, const fe *f, const fe *g) {
-  static const uint64_t p8_0 = 8 * (MASK51 - 18), p8_i = 8 * MASK51;
-  h->v[0] = f->v[0] + p8_0 - g->v[0];
-  for (int i = 1; i < 5; ++i) h->v[i] = f->v[i] + p8_i - g->v[i];
-  fe_carry(h);
+  static const uint64_t p16_0 = 16 * (MASK51 - 18), p16_i = 16 * MASK51;
+  h->v[0] = f->v[0] + p16_0 - g->v[0];
+  for (int i = 1; i < 5; ++i) h->v[i] = f->v[i] + p16_i - g->v[i];
+  fe_reduce(h);
 }
 
 static void fe_neg(fe *h, const fe *f) {
@@ -89,7 +103,28 @@ static void fe_mul(fe *h, const fe *f, const fe *g) {
   c = h->v[0] >> 51; h->v[0] &= MASK51; h->v[1] += c;
 }
 
-static void fe_sq(fe *h, const fe *f) { fe_mul(h, f, f); }
+/* Dedicated squaring (15 products instead of 25), as dalek's pow2k. */
+static void fe_sq(fe *h, const fe *f) {
+  const uint64_t f0 = f->v[0], f1 = f->v[1], f2 = f->v[2], f3 = f->v[3], f4 = f->v[4];
+  const uint64_t f0_2 = 2 * f0, f1_2 = 2 * f1, f1_38 = 38 * f1, f2_38 = 38 * f2, f3_38 = 38 * f3;
+  const uint64_t f3_19 = 19 * f3, f4_19 = 19 * f4;
+  u128 t0 = (u128)f0 * f0 + (u128)f1_38 * f4 + (u128)f2_38 * f3;
+  u128 t1 = (u128)f0_2 * f1 + (u128)f2_38 * f4 + (u128)f3_19 * f3;
+  u128 t2 = (u128)f0_2 * f2 + (u128)f1 * f1 + (u128)f3_38 * f4;
+  u128 t3 = (u128)f0_2 * f3 + (u128)f1_2 * f2 + (u128)f4_19 * f4;
+  u128 t4 = (u128)f0_2 * f4 + (u128)f1_2 * f3 + (u128)f2 * f2;
+  t1 += (uint64_t)(t0 >> 51);
+  t2 += (uint64_t)(t1 >> 51);
+  t3 += (uint64_t)(t2 >> 51);
+  t4 += (uint64_t)(t3 >> 51);
+  uint64_t c = (uint64_t)(t4 >> 51);
+  h->v[0] = ((uint64_t)t0 & MASK51) + 19 * c;
+  h->v[1] = (uint64_t)t1 & MASK51;
+  h->v[2] = (uint64_t)t2 & MASK51;
+  h->v[3] = (uint64_t)t3 & MASK51;
+  h->v[4] = (uint64_t)t4 & MASK51;
+  c = h->v[0] >> 51; h->v[0] &= MASK51; h->v[1] += c;
+}
 
 static void fe_sqn(fe *h, const fe *f, int n) {
   fe_sq(h, f);
@@ -922,4 +957,147 @@ void ntor_torsion_point(int i, uint8_t out32[32]) {
   ge_p3_0(&r);
   for (int k = 0; k < (i & 7); ++k) ge_add_p3(&r, &r, &T8);
   ge_tobytes(out32, &r);
+}
+
+/* ======================================================================== */
+/*  dalek's verify_batch as dalek computes it (CPU BASELINE ONLY)            */
+/* ======================================================================== */
+/* ed25519-dalek 1.0.1 verify_batch (crypto/src/lib.rs:218): random 128-bit z_i,
+ * one vartime multiscalar multiplication
+ *     [-sum z_i s_i]B + sum [z_i]R_i + sum [z_i k_i]A_i  ==  identity ?
+ * by Straus with width-5 NAF digits and per-point tables of odd multiples
+ * (curve25519-dalek's VartimeMultiscalarMul below 190 points).  This is the
+ * timing restatement behind bench.py's config-3 CPU baseline: the parity
+ * checker for batches stays ntor_ed25519_verify_batch (the deterministic
+ * rule of SURVEY A.3); both agree except on dalek's random class.
+ * z_i come from ChaCha20 keyed by `zkey` (stream = entry index) instead of
+ * merlin + thread_rng: the decision does not depend on which z are drawn
+ * outside that class. */
+int ntor_ed25519_verify_batch_dalek(const uint8_t *pk32, const uint8_t *sig64, uint64_t cnt,
+                                    const uint8_t *msg, uint64_t len, const uint8_t zkey[32]) {
+  ensure_consts();
+  if (cnt == 0) return 1;
+  const uint64_t npts = 2 * cnt + 1;
+  ge_p3 *pts = (ge_p3 *)malloc(npts * sizeof(ge_p3));
+  uint8_t *sc = (uint8_t *)calloc(npts, 32);
+  ge_cached *tab = (ge_cached *)malloc(npts * 8 * sizeof(ge_cached));
+  int8_t *naf = (int8_t *)malloc(npts * 257);
+  int ok = 1;
+  /* crypto/src/lib.rs:212-217: s check and A decode per entry, first failure -> Err */
+  for (uint64_t i = 0; i < cnt && ok; ++i) {
+    if (!ntor_sc_is_canonical(sig64 + 64 * i + 32) || !ge_frombytes(&pts[1 + cnt + i], pk32 + 32 * i)) ok = 0;
+  }
+  for (uint64_t i = 0; i < cnt && ok; ++i)
+    if (!ge_frombytes(&pts[1 + i], sig64 + 64 * i)) ok = 0;  /* R decompress */
+  if (ok) {
+    uint8_t zero[32] = {0}, bco[32] = {0};
+    pts[0] = BASE;
+    for (uint64_t i = 0; i < cnt; ++i) {
+      uint8_t z[32] = {0}, k[32];
+      ntor_chacha20_keystream(zkey, i, 0, z, 16);           /* 128-bit z_i */
+      memcpy(sc + 32 * (1 + i), z, 32);                     /* R_i: z_i */
+      hash_ram(k, sig64 + 64 * i, pk32 + 32 * i, msg, len);
+      sc_muladd(sc + 32 * (1 + cnt + i), z, k, zero);       /* A_i: z_i k_i mod L */
+      sc_muladd(bco, z, sig64 + 64 * i + 32, bco);          /* sum z_i s_i mod L */
+    }
+    /* B: L - bco (mod L) */
+    uint32_t l[8], b[8];
+    load_words(b, bco, 32);
+    memcpy(l, L_W, sizeof l);
+    int nz = 0;
+    for (int q = 0; q < 8; ++q) nz |= b[q] != 0;
+    if (nz) bn_sub(l, b, 8);
+    else memset(l, 0, sizeof l);
+    store_words(sc, l, 8);
+    for (uint64_t j = 0; j < npts; ++j) {
+      wnaf(naf + 257 * j, sc + 32 * j, 5);
+      ge_p3 P2, cur = pts[j];
+      ge_dbl_p3(&P2, &pts[j]);
+      for (int q = 0; q < 8; ++q) {  /* P, 3P, ..., 15P */
+        p3_to_cached(&tab[8 * j + q], &cur);
+        if (q < 7) ge_add_p3(&cur, &cur, &P2);
+      }
+    }
+    int top = 256;
+    for (; top >= 0; --top) {
+      uint64_t j = 0;
+      while (j < npts && naf[257 * j + top] == 0) ++j;
+      if (j < npts) break;
+    }
+    ge_p2 r;
+    ge_p2_0(&r);
+    ge_p1p1 t;
+    ge_p3 u;
+    for (int i = top; i >= 0; --i) {
+      ge_dbl(&t, &r);
+      for (uint64_t j = 0; j < npts; ++j) {
+        const int d = naf[257 * j + i];
+        if (!d) continue;
+        p1p1_to_p3(&u, &t);
+        ge_add_cached(&t, &u, &tab[8 * j + (d > 0 ? d : -d) / 2], d < 0);
+      }
+      p1p1_to_p2(&r, &t);
+    }
+    ok = fe_iszero(&r.X) && fe_eq(&r.Y, &r.Z);
+  }
+  free(pts);
+  free(sc);
+  free(tab);
+  free(naf);
+  return ok;
+}
+
+/* Certificate::verify over G certificates (primary/src/messages.rs:189-215),
+ * signature and digest work only (the committee stake/quorum checks are a few
+ * map lookups): header id == SHA-512(header preimage)[..32], header signature
+ * verify_strict, certificate digest SHA-512(id || round || origin)[..32], and
+ * dalek's verify_batch of the votes over it.  CPU BASELINE ONLY (bench.py
+ * config 3).  out: one byte per certificate. */
+typedef struct {
+  const uint8_t *hdr, *ids, *hpk, *hsig, *cpre, *vpk, *vsig;
+  const uint64_t *hoff, *hlen, *first;
+  const uint32_t *cnt;
+  uint64_t lo, hi;
+  uint8_t *out;
+} cjob;
+
+static void *cert_worker(void *p) {
+  cjob *j = (cjob *)p;
+  uint8_t zkey[32] = {0};
+  for (uint64_t g = j->lo; g < j->hi; ++g) {
+    uint8_t h[64], d[64];
+    ntor_sha512(j->hdr + j->hoff[g], j->hlen[g], h);
+    int ok = memcmp(h, j->ids + 32 * g, 32) == 0;
+    ok = ok && ntor_ed25519_verify_strict(j->hpk + 32 * g, j->hsig + 64 * g, j->ids + 32 * g, 32);
+    if (ok) {
+      ntor_sha512(j->cpre + 72 * g, 72, d);
+      memcpy(zkey, &g, sizeof g);
+      ok = ntor_ed25519_verify_batch_dalek(j->vpk + 32 * j->first[g], j->vsig + 64 * j->first[g], j->cnt[g], d, 32,
+                                           zkey);
+    }
+    j->out[g] = (uint8_t)ok;
+  }
+  return NULL;
+}
+
+void ntor_certificates_verify_many(const uint8_t *hdr, const uint64_t *hoff, const uint64_t *hlen,
+                                   const uint8_t *ids, const uint8_t *hpk, const uint8_t *hsig,
+                                   const uint8_t *cpre, const uint8_t *vpk, const uint8_t *vsig,
+                                   const uint64_t *first, const uint32_t *cnt, uint64_t G, uint8_t *out,
+                                   int nthreads) {
+  ensure_consts();
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  if ((uint64_t)nthreads > G) nthreads = G ? (int)G : 1;
+  pthread_t th[256];
+  cjob jobs[256];
+  for (int t = 0; t < nthreads; ++t) {
+    cjob c = {hdr, ids, hpk, hsig, cpre, vpk, vsig, hoff, hlen, first, cnt, G * t / nthreads, G * (t + 1) / nthreads,
+              out};
+    jobs[t] = c;
+    if (nthreads == 1) cert_worker(&jobs[t]);
+    else pthread_create(&th[t], NULL, cert_worker, &jobs[t]);
+  }
+  if (nthreads > 1)
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
 }

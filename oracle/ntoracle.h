@@ -70,6 +70,20 @@ void ntor_ed25519_verify_batch_groups(const uint8_t *pk32, const uint8_t *sig64,
                                       const uint8_t *msg32, uint64_t G, uint8_t *out_group_bitmap,
                                       uint8_t *out_sig_bitmap, int nthreads);
 
+/* CPU BASELINE ONLY (bench.py config 3): dalek's verify_batch as dalek computes
+ * it -- random 128-bit z_i (ChaCha20 keyed by zkey), one Straus/NAF-5 vartime
+ * multiscalar multiplication -- and Certificate::verify's signature + digest
+ * work over G certificates (header preimages at hoff/hlen in hdr, ids G*32,
+ * author keys hpk G*32, header signatures G*64, certificate digest preimages
+ * cpre G*72, votes vpk/vsig from first[g], cnt[g]).  out: 1 byte per certificate. */
+int ntor_ed25519_verify_batch_dalek(const uint8_t *pk32, const uint8_t *sig64, uint64_t cnt,
+                                    const uint8_t *msg, uint64_t len, const uint8_t zkey[32]);
+void ntor_certificates_verify_many(const uint8_t *hdr, const uint64_t *hoff, const uint64_t *hlen,
+                                   const uint8_t *ids, const uint8_t *hpk, const uint8_t *hsig,
+                                   const uint8_t *cpre, const uint8_t *vpk, const uint8_t *vsig,
+                                   const uint64_t *first, const uint32_t *cnt, uint64_t G, uint8_t *out,
+                                   int nthreads);
+
 /* Diagnostics used by the corpus generator (tests only). */
 /* 1 if the 32 bytes decode as a point under dalek decompress rules. */
 int ntor_point_decodes(const uint8_t p32[32]);

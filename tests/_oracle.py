@@ -89,6 +89,27 @@ class Oracle:
         return bool(self.lib.ntor_ed25519_verify_batch(pk, sg, ctypes.c_uint64(len(pks)), msg,
                                                        ctypes.c_uint64(len(msg))))
 
+    def verify_batch_dalek(self, pks, sigs, msg: bytes, zkey: bytes = bytes(32)) -> bool:
+        """dalek's randomized batch equation (CPU baseline form, see ntoracle.h)."""
+        self.lib.ntor_ed25519_verify_batch_dalek.restype = ctypes.c_int
+        return bool(self.lib.ntor_ed25519_verify_batch_dalek(b"".join(pks), b"".join(sigs), ctypes.c_uint64(len(pks)),
+                                                             msg, ctypes.c_uint64(len(msg)), zkey))
+
+    def certificates_verify_many(self, hdr, hoff, hlen, ids, hpk, hsig, cpre, vpk, vsig, first, cnt, nthreads=1):
+        """Certificate::verify signature + digest work per certificate (CPU baseline)."""
+        G = len(cnt)
+        out = np.zeros(max(G, 1), np.uint8)
+        a = [np.ascontiguousarray(x, np.uint8) for x in (hdr, ids, hpk, hsig, cpre, vpk, vsig)]
+        hoff = np.ascontiguousarray(hoff, np.uint64)
+        hlen = np.ascontiguousarray(hlen, np.uint64)
+        first = np.ascontiguousarray(first, np.uint64)
+        cnt = np.ascontiguousarray(cnt, np.uint32)
+        self.lib.ntor_certificates_verify_many(_ptr(a[0]), _ptr(hoff, _u64p), _ptr(hlen, _u64p), _ptr(a[1]),
+                                               _ptr(a[2]), _ptr(a[3]), _ptr(a[4]), _ptr(a[5]), _ptr(a[6]),
+                                               _ptr(first, _u64p), _ptr(cnt, _u32p), ctypes.c_uint64(G), _ptr(out),
+                                               ctypes.c_int(nthreads))
+        return out[:G]
+
     def batch_class(self, pk, sig, msg) -> int:
         return int(self.lib.ntor_ed25519_batch_class(pk, sig, msg, ctypes.c_uint64(len(msg))))
 

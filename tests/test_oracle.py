@@ -159,6 +159,81 @@ def test_corpus_batch_rule_and_class(oracle, corpus):
         assert oracle.batch_class(pk, sig, m) == int(corpus["batch_class"][i]), i
 
 
+def test_dalek_batch_equation_baseline(oracle, corpus):
+    """The CPU baseline's randomized Straus batch (dalek's own computation) gives
+    the deterministic A.3 verdict on every entry outside dalek's random class
+    (batch_class 2), on the reference's batch fixtures, and on 67-vote groups."""
+    for i in range(len(corpus["cat"])):
+        if int(corpus["batch_class"][i]) == 2:
+            continue
+        pk, sig, m = _entry(corpus, i)
+        assert oracle.verify_batch_dalek([pk], [sig], m) == bool(corpus["batch_rule"][i]), i
+    ref = _json("fixtures_reference.json")
+    d = oracle.digest(b"Hello, world!")
+    kp = [_kp(ref, i) for i in (3, 2, 1)]
+    sigs = [oracle.sign(s, p, d) for s, p in kp]
+    assert oracle.verify_batch_dalek([p for _, p in kp], sigs, d)          # crypto_tests.rs:79-94
+    assert not oracle.verify_batch_dalek([p for _, p in kp], sigs[:2] + [bytes(64)], d)  # :96-115
+    assert oracle.verify_batch_dalek([], [], d)
+    g = np.load(os.path.join(GOLD, "batch_groups.npz"))
+    ndet = 0
+    for i in range(len(g["cnt"])):
+        if not g["deterministic"][i]:
+            continue
+        f, c = int(g["first"][i]), int(g["cnt"][i])
+        got = oracle.verify_batch_dalek([x.tobytes() for x in g["pk"][f:f + c]], [x.tobytes() for x in g["sig"][f:f + c]],
+                                        g["msg32"][i].tobytes())
+        assert got == bool(g["expect"][i]), i
+        ndet += 1
+    assert ndet >= 40
+    seeds = [bytes([i + 1]) * 32 for i in range(67)]
+    pks = [oracle.pubkey(s) for s in seeds]
+    sg = [oracle.sign(s, p, d) for s, p in zip(seeds, pks)]
+    for z in (bytes(32), b"\x01" * 32):
+        assert oracle.verify_batch_dalek(pks, sg, d, z)
+        bad = list(sg)
+        bad[40] = bad[40][:40] + bytes([bad[40][40] ^ 1]) + bad[40][41:]
+        assert not oracle.verify_batch_dalek(pks, bad, d, z)
+
+
+def test_certificates_verify_many_baseline(oracle):
+    """Certificate::verify's signature + digest work (CPU baseline of config 3)."""
+    import struct
+    seeds = [bytes([i + 7]) * 32 for i in range(10)]
+    pks = [oracle.pubkey(s) for s in seeds]
+    hdr, hoff, hlen, ids, hpk, hsig, cpre, vpk, vsig, first, cnt, want = ([] for _ in range(12))
+    o = 0
+    for g in range(6):
+        a = g % 10
+        pre = pks[a] + struct.pack("<Q", g + 3) + bytes(range(40 + g))
+        hid = oracle.digest(pre)
+        hs = oracle.sign(seeds[a], pks[a], hid)
+        ok = True
+        if g == 2:
+            hs = hs[:33] + bytes([hs[33] ^ 1]) + hs[34:]
+            ok = False
+        cp = hid + struct.pack("<Q", g + 3) + pks[a]
+        cd = oracle.digest(cp)
+        first.append(len(vpk))
+        for v in range(7):
+            s = oracle.sign(seeds[v], pks[v], cd)
+            if g == 4 and v == 5:
+                s = bytes(32) + s[32:]
+                ok = False
+            vpk.append(pks[v])
+            vsig.append(s)
+        cnt.append(7)
+        if g == 5:
+            hid = bytes(32)
+            ok = False
+        hdr.append(pre); hoff.append(o); hlen.append(len(pre)); o += len(pre)
+        ids.append(hid); hpk.append(pks[a]); hsig.append(hs); cpre.append(cp); want.append(ok)
+    u8 = lambda xs: np.frombuffer(b"".join(xs), np.uint8)
+    got = oracle.certificates_verify_many(u8(hdr), hoff, hlen, u8(ids), u8(hpk), u8(hsig), u8(cpre), u8(vpk),
+                                          u8(vsig), first, cnt, nthreads=2)
+    assert got.astype(bool).tolist() == want
+
+
 def test_corpus_bulk_threads(oracle, corpus):
     got = oracle.verify_strict_many(corpus["pk"], corpus["sig"], corpus["msg"], corpus["off"],
                                     corpus["len"], nthreads=4)
