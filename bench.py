@@ -66,6 +66,7 @@ def parse():
     ap.add_argument("--no-certs", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-ingest", action="store_true")
+    ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--ingest-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-seconds of baseline work")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -320,6 +321,10 @@ def main():
                         "verdicts_equal_device_path": bool(np.array_equal(hv, got)),
                         "note": "nt_ed25519_verify_strict on the same cfg2 batch from pageable host buffers "
                                 "(608 MB over PCIe per call, copies of chunk c+1 under the kernels of chunk c)"}
+
+    # ------------------------------------------------- small calls: per-call latency
+    if not args.no_latency:
+        line["latency"] = bench_latency(be, pk_h, sig_h, msg_h, L)
 
     # ---------------------------------------------------------------- config 4: SHA-512 GB/s
     if not args.no_sha:
@@ -651,7 +656,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                     "ms_per_step": round(wall * 1e3 / steps, 3), "gpu_ms_per_step": round(kms, 3),
                     "mismatches_vs_expected": mism}
     ks.close()
-    if world == 1 and not args.no_cpu:
+    if world == 1 and not getattr(args, "no_cpu", False):
         out["cpu_baseline"] = cert_cpu_baseline(args, hdr, hlen, ids, tmp_pk, hsig, cpre, vpk, vsig, quorum, expect)
     return {"value": out["keyset"]["certs_per_s"], "unit": "certificates/s",
             "workload": "cfg3: %d certificates, committee n=%d, %d votes + 1 header signature each, "
@@ -664,6 +669,65 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                           "launches": "per step: 2 SHA-512 (header ids, certificate digests), 1 NT_MODE_MIXED key-cache "
                                       "verify (67 votes cofactorless + the header signature strict), 1 group AND"},
             **out}
+
+
+def bench_latency(be, pk_h, sig_h, msg_h, L):
+    """Per-call latency of the host entry points at the reference's call sizes
+    (SURVEY H3): Header/Vote::verify = one verify_strict over a 32-byte digest
+    (crypto/src/lib.rs:200-204), Certificate::verify's verify_batch = one group
+    of 67 votes (:206-219, primary/src/core.rs:349-411), a Processor call = one
+    508,052-B digest (worker/src/processor.rs:36-38).  p50 / p99 over repeated
+    calls from ordinary host buffers through the Python binding (ctypes: a few
+    us of the figure), with the small-call path off (every call on the GPU) and
+    in AUTO mode (below the crossover on host threads: csrc/cpu_lane.cpp)."""
+    import ntcrypto
+    rng = np.random.default_rng(11)
+    d = rng.integers(0, 256, 32, dtype=np.uint8)
+    seeds = rng.integers(0, 256, (67, 32), dtype=np.uint8)
+    pk67, sig67 = be.sign_batch(seeds, np.tile(d, 67), np.arange(67, dtype=np.uint64) * 32, np.full(67, 32, np.uint64))
+    one = (pk67[:1], sig67[:1], d, np.zeros(1, np.uint64), np.full(1, 32, np.uint64))
+    first, cnt = np.zeros(1, np.uint64), np.full(1, 67, np.uint32)
+    big = [rng.integers(0, 256, 508052, dtype=np.uint8).tobytes()]
+    cases = {
+        "verify_strict_n1": (lambda: be.verify_strict(*one), 200),
+        "verify_batch_1x67": (lambda: be.verify_batch_groups(pk67, sig67, first, cnt, d), 100),
+        "sha512_one_508052B": (lambda: be.digest_many(big), 30),
+    }
+    out = {"note": "per-call wall time (us) through the Python binding; gpu = small-call path off, "
+                   "auto = NT_SMALL_AUTO (calls below the crossover on host threads)"}
+    for mode, name in ((ntcrypto.NT_SMALL_OFF, "gpu"), (ntcrypto.NT_SMALL_AUTO, "auto")):
+        be.set_small_call_path(mode, 0)
+        for case, (fn, reps) in cases.items():
+            h0, g0 = be.call_counts()
+            fn()
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                fn()
+                ts.append((time.perf_counter() - t0) * 1e6)
+            h1, g1 = be.call_counts()
+            ts.sort()
+            out.setdefault(case, {})[name] = {"p50_us": round(ts[len(ts) // 2], 1),
+                                              "p99_us": round(ts[min(len(ts) - 1, int(len(ts) * 0.99))], 1),
+                                              "reps": reps, "host_calls": h1 - h0, "gpu_calls": g1 - g0}
+    # host-lane throughput of one thread (the small-call cost model's constants)
+    be.set_small_call_path(ntcrypto.NT_SMALL_ALWAYS, 1)
+    n = 64
+    offs = np.arange(n, dtype=np.uint64) * L
+    t0 = time.perf_counter()
+    be.verify_strict(pk_h[:n], sig_h[:n], msg_h[:n * L], offs, np.full(n, L, np.uint64))
+    per512 = (time.perf_counter() - t0) / n
+    t0 = time.perf_counter()
+    be.verify_strict(np.repeat(pk67[:1], n, 0), np.repeat(sig67[:1], n, 0), d, np.zeros(n, np.uint64),
+                     np.full(n, 32, np.uint64))
+    per32 = (time.perf_counter() - t0) / n
+    t0 = time.perf_counter()
+    be.digest_many(big)
+    sha_s = time.perf_counter() - t0
+    be.set_small_call_path(ntcrypto.NT_SMALL_OFF, 0)
+    out["host_lane_1thread"] = {"verify_us_msg32": round(per32 * 1e6, 1), "verify_us_msg512": round(per512 * 1e6, 1),
+                                "sha512_mb_per_s": round(508052 / sha_s / 1e6, 1)}
+    return out
 
 
 def cert_cpu_baseline(args, hdr, hlen, ids, hpk, hsig, cpre, vpk, vsig, quorum, expect):

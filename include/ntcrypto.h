@@ -134,6 +134,26 @@ int nt_ed25519_verify_batch_groups_keyset(nt_ctx *ctx, const nt_keyset *ks, cons
                                           const uint32_t *cnt, const uint8_t *msg32, uint64_t G,
                                           uint8_t *out_group_bitmap, uint8_t *out_sig_bitmap);
 
+/* ---- small-call path (SURVEY.md H3, §8(b) "CPU-fallback threshold") ------
+ * The reference calls verify once per header / vote, verify_batch once per
+ * certificate (primary/src/core.rs:349-411) and hashes one ~508 KB batch per
+ * Processor call (worker/src/processor.rs:36-38).  A GPU call that small costs
+ * a launch plus one lane's serial chain (a lone 508,052-B digest 16.8 ms on
+ * MI355X; a lone verify ~1.5 ms) -- more than the host needs.  With
+ * NT_SMALL_AUTO the host entry points run calls whose estimated host time is
+ * below their estimated GPU time on `threads` host threads, with the SAME
+ * arithmetic compiled for the host (csrc/cpu_lane.cpp; not the oracle); with
+ * NT_SMALL_ALWAYS every host entry point does (tests).  Default NT_SMALL_OFF:
+ * everything on the GPU.  The nt_dev_* entry points always run on the GPU.
+ * A context still requires a gfx950 device: this is a latency path, not a
+ * fallback.  threads <= 0: min(16, hardware threads). */
+#define NT_SMALL_OFF 0
+#define NT_SMALL_AUTO 1
+#define NT_SMALL_ALWAYS 2
+int nt_set_small_call_path(nt_ctx *ctx, int mode, int threads);
+/* Host entry-point calls served on host threads / on the GPU so far. */
+int nt_call_counts(const nt_ctx *ctx, uint64_t *host_calls, uint64_t *gpu_calls);
+
 /* ---- pinned host buffers ---------------------------------------------
  * Page-locked host memory for callers that stage large batches themselves
  * (the primary's wire ingestion).  Inputs that lie in such a buffer are

@@ -144,6 +144,68 @@ NT_HD NT_INLINE void fe_carry_wide(fe& out, uint64_t h[10]) {
   }
 }
 
+#if defined(NT_HOST_FAST_FE) && !defined(__HIP_DEVICE_COMPILE__)
+// ---- host lane only (csrc/cpu_lane.cpp, the small-call path) ----------------
+// On x86-64 a 64x64->128 multiply costs what a 32x32->64 one does, so the host
+// lane multiplies in radix 2^51: limbs 2k and 2k+1 of the radix-2^25.5 form
+// are exactly one radix-2^51 limb (weights 2^51k and 2^(51k+26)), giving 25
+// (mul) / 15 (sq) products instead of 100 / 55; the result is split back into
+// the 10-limb "R" form (even < 2^26, odd <= 2^25) every other function
+// expects.  Inputs: anything within the device contracts above (limbs < 2^28.6
+// -> radix-2^51 limbs < 2^54.6; every column < 2^115, carried in u128).
+typedef unsigned __int128 nt_u128;
+NT_HD NT_INLINE void fe51_pack(uint64_t F[5], const fe& f) {
+  for (int k = 0; k < 5; ++k) F[k] = (uint64_t)f.v[2 * k] + ((uint64_t)f.v[2 * k + 1] << 26);
+}
+NT_HD NT_INLINE void fe51_finish(fe& out, nt_u128 t0, nt_u128 t1, nt_u128 t2, nt_u128 t3, nt_u128 t4) {
+  const uint64_t M51 = (1ull << 51) - 1;
+  t1 += t0 >> 51; t0 &= M51;
+  t2 += t1 >> 51; t1 &= M51;
+  t3 += t2 >> 51; t2 &= M51;
+  t4 += t3 >> 51; t3 &= M51;
+  const nt_u128 c = t4 >> 51; t4 &= M51;
+  t0 += c * 19;
+  t1 += t0 >> 51; t0 &= M51;
+  const uint64_t r[5] = {(uint64_t)t0, (uint64_t)t1, (uint64_t)t2, (uint64_t)t3, (uint64_t)t4};
+  for (int k = 0; k < 5; ++k) {
+    out.v[2 * k] = (uint32_t)(r[k] & NT_M26);
+    out.v[2 * k + 1] = (uint32_t)(r[k] >> 26);
+  }
+}
+NT_HD NT_INLINE void fe_mul(fe& out, const fe& f, const fe& g) {
+  NT_COUNT_MUL();
+  uint64_t F[5], G[5];
+  fe51_pack(F, f);
+  fe51_pack(G, g);
+  const uint64_t g1 = 19 * G[1], g2 = 19 * G[2], g3 = 19 * G[3], g4 = 19 * G[4];
+#define NT_W(a, b) ((nt_u128)(a) * (b))
+  fe51_finish(out, NT_W(F[0], G[0]) + NT_W(F[1], g4) + NT_W(F[2], g3) + NT_W(F[3], g2) + NT_W(F[4], g1),
+              NT_W(F[0], G[1]) + NT_W(F[1], G[0]) + NT_W(F[2], g4) + NT_W(F[3], g3) + NT_W(F[4], g2),
+              NT_W(F[0], G[2]) + NT_W(F[1], G[1]) + NT_W(F[2], G[0]) + NT_W(F[3], g4) + NT_W(F[4], g3),
+              NT_W(F[0], G[3]) + NT_W(F[1], G[2]) + NT_W(F[2], G[1]) + NT_W(F[3], G[0]) + NT_W(F[4], g4),
+              NT_W(F[0], G[4]) + NT_W(F[1], G[3]) + NT_W(F[2], G[2]) + NT_W(F[3], G[1]) + NT_W(F[4], G[0]));
+}
+NT_HD NT_INLINE void fe51_square(fe& out, const fe& f) {
+  uint64_t F[5];
+  fe51_pack(F, f);
+  const uint64_t f0_2 = 2 * F[0], f1_2 = 2 * F[1], f1_38 = 38 * F[1], f2_38 = 38 * F[2], f3_38 = 38 * F[3];
+  const uint64_t f3_19 = 19 * F[3], f4_19 = 19 * F[4];
+  fe51_finish(out, NT_W(F[0], F[0]) + NT_W(f1_38, F[4]) + NT_W(f2_38, F[3]),
+              NT_W(f0_2, F[1]) + NT_W(f2_38, F[4]) + NT_W(f3_19, F[3]),
+              NT_W(f0_2, F[2]) + NT_W(F[1], F[1]) + NT_W(f3_38, F[4]),
+              NT_W(f0_2, F[3]) + NT_W(f1_2, F[2]) + NT_W(f4_19, F[4]),
+              NT_W(f0_2, F[4]) + NT_W(f1_2, F[3]) + NT_W(F[2], F[2]));
+#undef NT_W
+}
+NT_HD NT_INLINE void fe_sq_wide(fe& out, const fe& f) {
+  NT_COUNT_SQ();
+  fe51_square(out, f);
+}
+NT_HD NT_INLINE void fe_sq(fe& out, const fe& f) {
+  NT_COUNT_SQ();
+  fe51_square(out, f);
+}
+#else
 // h = f * g.  Each partial product is one v_mad_u64_u32.
 NT_HD NT_INLINE void fe_mul(fe& out, const fe& f, const fe& g) {
   NT_COUNT_MUL();
@@ -232,6 +294,8 @@ NT_HD NT_INLINE void fe_sq(fe& out, const fe& f) {
   fe_carry_wide(out, h);
   NT_MUL_FENCE();
 }
+
+#endif  // NT_HOST_FAST_FE
 
 // Repeated squaring; kept as a loop (not unrolled) so the exponentiation chains
 // stay small in the instruction cache.

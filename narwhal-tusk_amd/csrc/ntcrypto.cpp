@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -20,6 +22,7 @@
 #include <vector>
 
 #include "../../include/ntcrypto.h"
+#include "cpu_lane.hpp"
 #include "kernels.hpp"
 
 namespace {
@@ -255,11 +258,16 @@ struct Device {
 
 struct nt_ctx {
   std::vector<std::unique_ptr<Device>> devs;
+  // small-call path (cpu_lane.hpp): NT_SMALL_OFF / AUTO / ALWAYS, host threads
+  std::atomic<int> small_mode{NT_SMALL_OFF};
+  std::atomic<int> small_threads{1};
+  std::atomic<uint64_t> calls_host{0}, calls_gpu{0};
 };
 
 struct nt_keyset {
   nt_ctx* ctx = nullptr;
   uint32_t nkeys = 0;
+  std::vector<uint8_t> enc;     // host copy of the key encodings (small-call path)
   int bits = 0;                 // comb digit width of every key (nt::kKeyCombWide / kKeyCombNarrow)
   std::vector<uint32_t> flags;  // host copy of kKey* bits
   struct PerDev {
@@ -340,6 +348,22 @@ int nt_init_devices(nt_ctx** out, const int* ordinals, int n) {
 void nt_free(nt_ctx* ctx) { delete ctx; }
 
 int nt_num_devices(const nt_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+int nt_set_small_call_path(nt_ctx* ctx, int mode, int threads) {
+  if (!ctx || mode < NT_SMALL_OFF || mode > NT_SMALL_ALWAYS) return NT_EINVAL;
+  if (threads <= 0) threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  ctx->small_threads = threads;
+  if (mode != NT_SMALL_OFF) nt::cpu::init(threads);
+  ctx->small_mode = mode;
+  return NT_OK;
+}
+
+int nt_call_counts(const nt_ctx* ctx, uint64_t* host_calls, uint64_t* gpu_calls) {
+  if (!ctx) return NT_EINVAL;
+  if (host_calls) *host_calls = ctx->calls_host.load();
+  if (gpu_calls) *gpu_calls = ctx->calls_gpu.load();
+  return NT_OK;
+}
 
 void* nt_host_alloc(uint64_t bytes) {
   void* p = nullptr;
@@ -606,6 +630,107 @@ Device* dev_of(nt_ctx* ctx, int dev) {
   return ctx->devs[dev].get();
 }
 
+// ---- small-call path (cpu_lane.hpp) -----------------------------
+// Cost model of one host entry-point call, from the `latency` block of
+// bench.py on MI355X (profiles/r02/latency_*.json).  A GPU call below one
+// round of resident waves costs a fixed floor (launch + copies + the two
+// signatures every lane of the verify kernel runs); the digest kernel's time
+// is set by its LONGEST message (one lane's serial chain) plus the PCIe copy.
+// NT_SMALL_* environment variables override the constants (A/B runs).
+double env_or(const char* name, double dflt) {
+  const char* e = std::getenv(name);
+  return e && *e ? std::atof(e) : dflt;
+}
+struct SmallModel {
+  double cpu_verify_us, gpu_verify_us, cpu_sha_mbs, gpu_lane_mbs, gpu_call_us, pcie_gbs, spawn_us;
+  SmallModel()
+      : cpu_verify_us(env_or("NT_SMALL_CPU_VERIFY_US", 75.0)),
+        gpu_verify_us(env_or("NT_SMALL_GPU_VERIFY_US", 1700.0)),
+        cpu_sha_mbs(env_or("NT_SMALL_CPU_SHA_MBS", 450.0)),
+        gpu_lane_mbs(env_or("NT_SMALL_GPU_LANE_MBS", 30.0)),
+        gpu_call_us(env_or("NT_SMALL_GPU_CALL_US", 60.0)),
+        pcie_gbs(env_or("NT_SMALL_PCIE_GBS", 20.0)),
+        spawn_us(env_or("NT_SMALL_SPAWN_US", 40.0)) {}
+};
+const SmallModel& small_model() {
+  static const SmallModel m;
+  return m;
+}
+
+int small_threads(const nt_ctx* ctx, uint64_t items) {
+  const uint64_t t = (uint64_t)std::max(1, ctx->small_threads.load());
+  return (int)std::max<uint64_t>(1, std::min(t, items));
+}
+
+// estimated host time of `nsig` verifications on the context's host threads
+bool small_verify(nt_ctx* ctx, uint64_t nsig) {
+  const int mode = ctx->small_mode.load();
+  if (mode == NT_SMALL_ALWAYS) return true;
+  if (mode != NT_SMALL_AUTO || !nt::cpu::ready()) return false;
+  const SmallModel& m = small_model();
+  const int T = small_threads(ctx, nsig);
+  const double cpu = std::ceil((double)nsig / T) * m.cpu_verify_us + (T > 1 ? m.spawn_us : 0.0);
+  return cpu < m.gpu_verify_us;
+}
+
+bool small_sha(nt_ctx* ctx, uint64_t n, const uint64_t* len) {
+  const int mode = ctx->small_mode.load();
+  if (mode == NT_SMALL_ALWAYS) return true;
+  if (mode != NT_SMALL_AUTO) return false;
+  const SmallModel& m = small_model();
+  uint64_t total = 0, mx = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    total += len[i];
+    mx = std::max(mx, len[i]);
+  }
+  const int T = small_threads(ctx, n);
+  const double cpu = std::max((double)mx, (double)total / T) / m.cpu_sha_mbs + (T > 1 ? m.spawn_us : 0.0);
+  const double gpu = m.gpu_call_us + (double)mx / m.gpu_lane_mbs + (double)total / (m.pcie_gbs * 1e3);
+  return cpu < gpu;
+}
+
+void bits_from_bytes(uint8_t* bitmap, const std::vector<uint8_t>& v) {
+  std::memset(bitmap, 0, (v.size() + 7) / 8);
+  for (size_t i = 0; i < v.size(); ++i)
+    if (v[i]) bitmap[i >> 3] |= (uint8_t)(1u << (i & 7));
+}
+
+// certificate groups on host threads: per-signature rule, AND per group.
+// key(e, A) writes signature e's key encoding to A and returns its mode
+// (kStrict / kCofactorless) or -1 for "no such key" (reject).
+template <class KeyOf>
+int host_groups(nt_ctx* ctx, const uint8_t* sig64, const uint64_t* first, const uint32_t* cnt, const uint8_t* msg32,
+                uint64_t G, uint8_t* out_group_bitmap, uint8_t* out_sig_bitmap, KeyOf&& key) {
+  std::vector<uint64_t> gbase(G + 1, 0);
+  uint64_t nsig_total = 0;
+  for (uint64_t g = 0; g < G; ++g) {
+    gbase[g + 1] = gbase[g] + cnt[g];
+    nsig_total = std::max(nsig_total, first[g] + cnt[g]);
+  }
+  const uint64_t m = gbase[G];
+  std::vector<uint8_t> ok(m, 0);
+  nt::cpu::parallel_for(m, small_threads(ctx, m), [&](uint64_t e) {
+    const uint64_t g = (uint64_t)(std::upper_bound(gbase.begin(), gbase.end(), e) - gbase.begin()) - 1;
+    const uint64_t s = first[g] + (e - gbase[g]);
+    uint8_t A[32];
+    const int mode = key(s, A);
+    ok[e] = mode >= 0 && nt::cpu::verify(mode, A, sig64 + 64 * s, msg32 + 32 * g, 32);
+  });
+  std::memset(out_group_bitmap, 0, (G + 7) / 8);
+  if (out_sig_bitmap) std::memset(out_sig_bitmap, 0, (nsig_total + 7) / 8);
+  for (uint64_t g = 0; g < G; ++g) {
+    bool all = true;
+    for (uint64_t e = gbase[g]; e < gbase[g + 1]; ++e) {
+      all = all && ok[e];
+      const uint64_t s = first[g] + (e - gbase[g]);
+      if (out_sig_bitmap && ok[e]) out_sig_bitmap[s >> 3] |= (uint8_t)(1u << (s & 7));
+    }
+    if (all) out_group_bitmap[g >> 3] |= (uint8_t)(1u << (g & 7));
+  }
+  ctx->calls_host++;
+  return NT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -614,6 +739,14 @@ int nt_sha512_trunc32(nt_ctx* ctx, const uint8_t* data, const uint64_t* off, con
                       uint64_t n, uint8_t* out32) {
   if (!ctx || (n && (!off || !len || !out32))) return NT_EINVAL;
   if (n == 0) return NT_OK;
+  if (small_sha(ctx, n, len)) {
+    nt::cpu::parallel_for(n, small_threads(ctx, n), [&](uint64_t i) {
+      nt::cpu::sha512_trunc32(data + off[i], len[i], out32 + 32 * i);
+    });
+    ctx->calls_host++;
+    return NT_OK;
+  }
+  ctx->calls_gpu++;
   return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
     const uint64_t m = hi - lo;
     // a launch's time is set by its longest message: chunks of >= 64k messages
@@ -641,6 +774,16 @@ int nt_ed25519_verify_strict(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* si
                              uint64_t n, uint8_t* out_bitmap) {
   if (!ctx || (n && (!pk32 || !sig64 || !off || !len || !out_bitmap))) return NT_EINVAL;
   if (n == 0) return NT_OK;
+  if (small_verify(ctx, n)) {
+    std::vector<uint8_t> ok(n);
+    nt::cpu::parallel_for(n, small_threads(ctx, n), [&](uint64_t i) {
+      ok[i] = nt::cpu::verify(nt::kStrict, pk32 + 32 * i, sig64 + 64 * i, msg + off[i], len[i]);
+    });
+    bits_from_bytes(out_bitmap, ok);
+    ctx->calls_host++;
+    return NT_OK;
+  }
+  ctx->calls_gpu++;
   return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
     const uint64_t m = hi - lo, words = (m + 63) / 64;
     const auto ch = plan_chunks(m, pipe_round(nt::verify_round_sigs(dv.cus)));
@@ -857,6 +1000,17 @@ int nt_ed25519_verify_batch_groups(nt_ctx* ctx, const uint8_t* pk32, const uint8
                                    uint8_t* out_sig_bitmap) {
   if (!ctx || (G && (!first || !cnt || !msg32 || !out_group_bitmap))) return NT_EINVAL;
   if (G == 0) return NT_OK;
+  uint64_t m = 0;
+  for (uint64_t g = 0; g < G; ++g) m += cnt[g];
+  if (small_verify(ctx, m)) {
+    if (m && (!pk32 || !sig64)) return NT_EINVAL;
+    return host_groups(ctx, sig64, first, cnt, msg32, G, out_group_bitmap, out_sig_bitmap,
+                       [&](uint64_t s, uint8_t A[32]) {
+                         std::memcpy(A, pk32 + 32 * s, 32);
+                         return (int)nt::kCofactorless;
+                       });
+  }
+  ctx->calls_gpu++;
   return verify_groups(ctx, nullptr, 32, pk32, sig64, first, cnt, msg32, G, out_group_bitmap, out_sig_bitmap);
 }
 
@@ -915,6 +1069,20 @@ static int keyset_comb_bits(nt_ctx* ctx, uint32_t nkeys) {
   return nt::kKeyCombWide;
 }
 
+// Small-call path: key encoding and check mode of one key-cache entry, as
+// the key-cache kernel's loader decodes key_idx (k_keyset.inc KsLoader): in
+// NT_MODE_MIXED bit 31 selects strict; an index >= nkeys is no key (-1, reject).
+static int keyset_key(const nt_keyset* ks, int mode, uint32_t kraw, uint8_t A[32]) {
+  int m = mode == NT_MODE_STRICT ? nt::kStrict : nt::kCofactorless;
+  if (mode == NT_MODE_MIXED) {
+    m = (kraw & NT_KEY_STRICT_BIT) ? nt::kStrict : nt::kCofactorless;
+    kraw &= ~NT_KEY_STRICT_BIT;
+  }
+  if (kraw >= ks->nkeys) return -1;
+  std::memcpy(A, ks->enc.data() + 32ull * kraw, 32);
+  return m;
+}
+
 int nt_keyset_create(nt_ctx* ctx, const uint8_t* pk32, uint32_t nkeys, nt_keyset** out) {
   if (!ctx || !out || (nkeys && !pk32)) return NT_EINVAL;
   *out = nullptr;
@@ -923,6 +1091,7 @@ int nt_keyset_create(nt_ctx* ctx, const uint8_t* pk32, uint32_t nkeys, nt_keyset
   ks->nkeys = nkeys;
   ks->bits = keyset_comb_bits(ctx, nkeys);
   ks->flags.assign(nkeys, 0);
+  if (nkeys) ks->enc.assign(pk32, pk32 + 32ull * nkeys);
   ks->dev.resize(ctx->devs.size());
   for (size_t di = 0; di < ctx->devs.size(); ++di) {
     Device& dv = *ctx->devs[di];
@@ -972,6 +1141,18 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
     return NT_EINVAL;
   if (n && (!key_idx || !sig64 || !off || !len || !out_bitmap)) return NT_EINVAL;
   if (n == 0) return NT_OK;
+  if (small_verify(ctx, n)) {
+    std::vector<uint8_t> ok(n);
+    nt::cpu::parallel_for(n, small_threads(ctx, n), [&](uint64_t i) {
+      uint8_t A[32];
+      const int m = keyset_key(ks, mode, key_idx[i], A);
+      ok[i] = m >= 0 && nt::cpu::verify(m, A, sig64 + 64 * i, msg + off[i], len[i]);
+    });
+    bits_from_bytes(out_bitmap, ok);
+    ctx->calls_host++;
+    return NT_OK;
+  }
+  ctx->calls_gpu++;
   return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
     const auto& pd = ks->dev[dev_index(ctx, dv)];
     const uint64_t m = hi - lo, words = (m + 63) / 64;
@@ -1019,6 +1200,14 @@ int nt_ed25519_verify_batch_groups_keyset(nt_ctx* ctx, const nt_keyset* ks, cons
   if (!ctx || !ks || ks->ctx != ctx) return NT_EINVAL;
   if (G && (!first || !cnt || !msg32 || !out_group_bitmap)) return NT_EINVAL;
   if (G == 0) return NT_OK;
+  uint64_t m = 0;
+  for (uint64_t g = 0; g < G; ++g) m += cnt[g];
+  if (small_verify(ctx, m)) {
+    if (m && (!key_idx || !sig64)) return NT_EINVAL;
+    return host_groups(ctx, sig64, first, cnt, msg32, G, out_group_bitmap, out_sig_bitmap,
+                       [&](uint64_t s, uint8_t A[32]) { return keyset_key(ks, NT_MODE_COFACTORLESS, key_idx[s], A); });
+  }
+  ctx->calls_gpu++;
   return verify_groups(ctx, ks, 4, (const uint8_t*)key_idx, sig64, first, cnt, msg32, G, out_group_bitmap,
                        out_sig_bitmap);
 }

@@ -79,6 +79,9 @@ NT_HD NT_INLINE uint64_t bitop3_64(uint64_t x, uint64_t y, uint64_t z) {
       __builtin_amdgcn_bitop3_b32((uint32_t)(x >> 32), (uint32_t)(y >> 32), (uint32_t)(z >> 32), TT);
   return ((uint64_t)hi << 32) | lo;
 #else
+  if constexpr (TT == 0x96) return x ^ y ^ z;                       // XOR3
+  if constexpr (TT == 0xE8) return (x & y) | (z & (x | y));         // MAJ
+  if constexpr (TT == 0xCA) return z ^ (x & (y ^ z));               // CH
   uint64_t r = 0;
   for (int i = 0; i < 8; ++i)
     if ((TT >> i) & 1) {

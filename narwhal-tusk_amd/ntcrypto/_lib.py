@@ -16,6 +16,9 @@ NT_MODE_STRICT = 0
 NT_MODE_COFACTORLESS = 1
 NT_MODE_MIXED = 2             # key-cache only: key_idx bit 31 = strict
 NT_KEY_STRICT_BIT = 0x80000000
+NT_SMALL_OFF = 0              # small-call path (include/ntcrypto.h): everything on the GPU
+NT_SMALL_AUTO = 1             # calls below the host/GPU crossover on host threads
+NT_SMALL_ALWAYS = 2           # every host entry point on host threads (tests)
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -29,7 +32,7 @@ EXPORTED = [
     "nt_ed25519_sign_batch", "nt_ed25519_keypair_batch", "nt_dev_sha512_trunc32",
     "nt_dev_ed25519_verify", "nt_dev_group_and", "nt_dev_ed25519_sign", "nt_keyset_create",
     "nt_keyset_free", "nt_keyset_flags", "nt_keyset_info", "nt_ed25519_verify_keyset", "nt_ed25519_verify_batch_groups_keyset",
-    "nt_dev_ed25519_verify_keyset", "nt_host_alloc", "nt_host_free",
+    "nt_dev_ed25519_verify_keyset", "nt_host_alloc", "nt_host_free", "nt_set_small_call_path", "nt_call_counts",
 ]
 
 
@@ -81,6 +84,8 @@ def load_library(path=None):
                                                           _u8p]
     lib.nt_dev_ed25519_verify_keyset.argtypes = [_vp, _vp, ctypes.c_int, _vp, ctypes.c_int, _vp, _vp, _vp, _vp,
                                                  _vp, _u64, _vp]
+    lib.nt_set_small_call_path.argtypes = [_vp, ctypes.c_int, ctypes.c_int]
+    lib.nt_call_counts.argtypes = [_vp, _u64p, _u64p]
     _lib = lib
     return lib
 
@@ -133,6 +138,17 @@ class Backend:
     @property
     def num_devices(self):
         return self.lib.nt_num_devices(self.ctx)
+
+    def set_small_call_path(self, mode=NT_SMALL_AUTO, threads=0):
+        """Small calls on host threads (include/ntcrypto.h)."""
+        _check(self.lib.nt_set_small_call_path(self.ctx, int(mode), int(threads)), "nt_set_small_call_path")
+
+    def call_counts(self):
+        """(host-lane calls, GPU calls) of the host entry points so far."""
+        h = np.zeros(1, np.uint64)
+        g = np.zeros(1, np.uint64)
+        _check(self.lib.nt_call_counts(self.ctx, _p(h, _u64p), _p(g, _u64p)), "nt_call_counts")
+        return int(h[0]), int(g[0])
 
     # ---- SHA-512 ----
     def sha512_trunc32(self, data, off, ln):

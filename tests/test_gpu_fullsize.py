@@ -101,7 +101,7 @@ def test_cfg2_million_verifies(env):
 def test_cfg3_hundred_thousand_certificates(env):
     sys.path.insert(0, ROOT)
     import bench
-    args = types.SimpleNamespace(committee=100, certs=100_000, steps=1, warmup=1)
+    args = types.SimpleNamespace(committee=100, certs=100_000, steps=1, warmup=1, no_cpu=True)
     with env.torch.cuda.stream(env.stream):
         res = bench.bench_certs(args, env.torch, env.dev, env.be, env.sp, env.stream, 1, 0,
                                 lambda: env.torch.cuda.synchronize(env.dev), lambda x: x)
