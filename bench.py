@@ -326,6 +326,11 @@ def main():
     if not args.no_latency:
         line["latency"] = bench_latency(be, pk_h, sig_h, msg_h, L)
 
+    # ----------------------- worker digest batching (§8(f).3) and device-slot contention
+    if not args.no_latency and world == 1:
+        line["digest_batcher"] = bench_batcher()
+        line["contention"] = bench_contention(ntcrypto, local)
+
     # ---------------------------------------------------------------- config 4: SHA-512 GB/s
     if not args.no_sha:
         line["sha512"] = bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_ranks)
@@ -727,6 +732,118 @@ def bench_latency(be, pk_h, sig_h, msg_h, L):
     be.set_small_call_path(ntcrypto.NT_SMALL_OFF, 0)
     out["host_lane_1thread"] = {"verify_us_msg32": round(per32 * 1e6, 1), "verify_us_msg512": round(per512 * 1e6, 1),
                                 "sha512_mb_per_s": round(508052 / sha_s / 1e6, 1)}
+    return out
+
+
+def bench_batcher(per_stream=64, size=508052):
+    """worker::DigestBatcher (SURVEY §8(f).3): the worker's two Processor streams
+    (own batches / others' batches, worker/src/worker.rs:182-188, 227-233) each
+    push `per_stream` real-size batches from their own thread, keeping them in
+    flight and awaiting the results in order; the batcher hashes what is queued
+    in one nt_sha512_trunc32 call per flush (1 ms age / 64 MB / 4096 batches).
+    Per-batch latency = submit -> digest.  GPU vs the small-call path (AUTO)."""
+    import hashlib
+    import threading
+    from ntcrypto import narwhal as N
+    rng = np.random.default_rng(21)
+    jobs = {own: [rng.integers(0, 256, size, dtype=np.uint8).tobytes() for _ in range(per_stream)]
+            for own in (True, False)}
+    out = {"workload": "2 Processor streams x %d batches of %d B, pipelined" % (per_stream, size)}
+    for mode, name in ((0, "gpu"), (1, "auto")):
+        N.set_small_call_path(mode, 0)
+        b = N.DigestBatcher(max_bytes=64 << 20, max_batches=4096, max_delay_us=1000)
+        lat, res = {True: [], False: []}, {}
+
+        def stream(own):
+            t_sub, tickets = [], []
+            for x in jobs[own]:
+                t_sub.append(time.perf_counter())
+                tickets.append(b.submit(0, own, x))
+            got = []
+            for t0, t in zip(t_sub, tickets):
+                got.append(b.wait(t)[0])
+                lat[own].append(time.perf_counter() - t0)
+            res[own] = got
+
+        b.process(0, True, jobs[True][0])  # warm-up (contexts, pinned arenas)
+        st0 = b.stats()
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=stream, args=(own,)) for own in (True, False)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        wall = time.perf_counter() - t0
+        st = b.stats()
+        b.close()
+        ok = all(d == hashlib.sha512(x).digest()[:32] for own in (True, False) for x, d in zip(jobs[own], res[own]))
+        ls = sorted(lat[True] + lat[False])
+        nb = 2 * per_stream
+        out[name] = {"batches_per_s": round(nb / wall, 1), "gb_per_s": round(nb * size / wall / 1e9, 3),
+                     "latency_p50_ms": round(ls[len(ls) // 2] * 1e3, 3),
+                     "latency_p99_ms": round(ls[min(len(ls) - 1, int(len(ls) * 0.99))] * 1e3, 3),
+                     "flushes": st["flushes"] - st0["flushes"], "digests_match_hashlib": bool(ok)}
+    N.set_small_call_path(0)
+    return out
+
+
+def bench_contention(ntcrypto, device, reps=40):
+    """Device-lock contention (one context shared by a worker and a primary,
+    SURVEY §3.5): a Core-shaped call -- verify_batch of a drained batch of 100
+    certificates x 67 votes -- timed alone and while another thread keeps the
+    same context busy with Processor-shaped digest flushes (64 x 508,052 B on
+    the GPU).  NT_SLOTS=1: one execution slot per device (the call waits for the
+    flush to finish); default NT_SLOTS=2: a second slot runs it concurrently."""
+    import threading
+    rng = np.random.default_rng(31)
+    G, q = 100, 67
+    seeds = rng.integers(0, 256, (q, 32), dtype=np.uint8)
+    dig = rng.integers(0, 256, (G, 32), dtype=np.uint8)
+    big = rng.integers(0, 256, 64 * 508052, dtype=np.uint8)
+    boff = np.arange(64, dtype=np.uint64) * 508052
+    blen = np.full(64, 508052, np.uint64)
+    out = {"call": "verify_batch_groups: %d certificates x %d votes (GPU path)" % (G, q),
+           "background": "nt_sha512_trunc32 of 64 x 508,052 B in a loop (GPU path)"}
+    saved = os.environ.get("NT_SLOTS")
+    for slots in (1, 2):
+        os.environ["NT_SLOTS"] = str(slots)
+        be = ntcrypto.Backend(device=device)
+        try:
+            msgs = np.repeat(dig, q, axis=0).reshape(-1)
+            pk, sig = be.sign_batch(np.tile(seeds, (G, 1)), msgs, np.arange(G * q, dtype=np.uint64) * 32,
+                                    np.full(G * q, 32, np.uint64))
+            first = np.arange(G, dtype=np.uint64) * q
+            cnt = np.full(G, q, np.uint32)
+
+            def call():
+                t0 = time.perf_counter()
+                ok = be.verify_batch_groups(pk, sig, first, cnt, dig.reshape(-1))
+                assert ok.all()
+                return (time.perf_counter() - t0) * 1e3
+
+            call()
+            alone = sorted(call() for _ in range(reps))
+            stop = threading.Event()
+
+            def background():
+                while not stop.is_set():
+                    be.sha512_trunc32(big, boff, blen)
+
+            th = threading.Thread(target=background)
+            th.start()
+            time.sleep(0.05)
+            busy = sorted(call() for _ in range(reps))
+            stop.set()
+            th.join()
+        finally:
+            be.close()
+        out["slots_%d" % slots] = {"alone_p50_ms": round(alone[reps // 2], 3), "alone_p99_ms": round(alone[-1], 3),
+                                   "with_digests_p50_ms": round(busy[reps // 2], 3),
+                                   "with_digests_p99_ms": round(busy[-1], 3)}
+    if saved is None:
+        os.environ.pop("NT_SLOTS", None)
+    else:
+        os.environ["NT_SLOTS"] = saved
     return out
 
 

@@ -6,8 +6,13 @@
 
 #include <stdint.h>
 
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 // The device headers are compiled here into a namespace of their own (nt_lane),
@@ -68,7 +73,96 @@ void build(int threads) {
   g_comb = comb;
 }
 
+// Persistent workers for parallel_for_fn: a small call must not pay a thread
+// creation per item (16 std::thread spawns cost ~400 us, more than a 67-vote
+// certificate's verification on 16 threads).  A call enqueues a job; workers
+// and the caller claim its items one at a time under the pool lock.
+struct Job {
+  const std::function<void(uint64_t)>* fn;
+  uint64_t n;
+  uint64_t next = 0;                // next unclaimed item (pool lock)
+  std::atomic<uint64_t> done{0};    // finished items
+};
+
+class Pool {
+ public:
+  explicit Pool(int workers) {
+    for (int t = 0; t < workers; ++t) th_.emplace_back([this] { loop(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void run(uint64_t n, const std::function<void(uint64_t)>& fn) {
+    Job j;
+    j.fn = &fn;
+    j.n = n;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.push_back(&j);
+    }
+    cv_.notify_all();
+    for (;;) {  // the caller works on its own job
+      uint64_t i;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (j.next >= n) break;
+        i = j.next++;
+        if (j.next == n) erase(&j);
+      }
+      fn(i);
+      j.done.fetch_add(1);
+    }
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return j.done.load() == n; });
+  }
+
+ private:
+  void erase(Job* j) {
+    for (auto it = q_.begin(); it != q_.end(); ++it)
+      if (*it == j) {
+        q_.erase(it);
+        return;
+      }
+  }
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      if (stop_) return;
+      Job* j = q_.front();
+      const uint64_t i = j->next++, n = j->n;
+      if (j->next == n) q_.pop_front();
+      const std::function<void(uint64_t)>* fn = j->fn;
+      lk.unlock();
+      (*fn)(i);
+      // the last access to *j: once done == n its caller may return
+      const bool last = j->done.fetch_add(1) + 1 == n;
+      lk.lock();
+      if (last) done_cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::deque<Job*> q_;
+  std::vector<std::thread> th_;
+  bool stop_ = false;
+};
+
+Pool& pool(int threads) {
+  static Pool p(std::max(1, std::min(64, threads) - 1));
+  return p;
+}
+
 }  // namespace
+
+void parallel_for_fn(uint64_t n, int threads, const std::function<void(uint64_t)>& fn) {
+  pool(threads).run(n, fn);
+}
 
 void init(int threads) {
   std::call_once(g_once, [threads] { build(threads); });

@@ -20,6 +20,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 
 namespace nt {
 namespace cpu {
@@ -35,29 +36,18 @@ void sha512_trunc32(const uint8_t* msg, uint64_t len, uint8_t out32[32]);
 // verify_batch under SURVEY A.3).  Requires init().
 bool verify(int mode, const uint8_t pk32[32], const uint8_t sig64[64], const uint8_t* msg, uint64_t len);
 
-// fn(i) for i in [0, n) on up to `threads` threads (the caller's thread included).
+// fn(i) for i in [0, n) on the lane's persistent worker pool plus the calling
+// thread (threads <= 1 or n <= 1: inline).  Safe to call from several threads
+// at once: each call is a job the pool's workers share with its caller.
+void parallel_for_fn(uint64_t n, int threads, const std::function<void(uint64_t)>& fn);
 template <class F>
-void parallel_for(uint64_t n, int threads, F&& fn);
-
-}  // namespace cpu
-}  // namespace nt
-
-#include <thread>
-#include <vector>
-
-template <class F>
-void nt::cpu::parallel_for(uint64_t n, int threads, F&& fn) {
-  const uint64_t T = threads < 1 ? 1 : (uint64_t)threads < n ? (uint64_t)threads : n;
-  if (T <= 1) {
+void parallel_for(uint64_t n, int threads, F&& fn) {
+  if (threads <= 1 || n <= 1) {
     for (uint64_t i = 0; i < n; ++i) fn(i);
     return;
   }
-  auto work = [&](uint64_t t) {
-    for (uint64_t i = n * t / T; i < n * (t + 1) / T; ++i) fn(i);
-  };
-  std::vector<std::thread> th;
-  th.reserve(T - 1);
-  for (uint64_t t = 1; t < T; ++t) th.emplace_back(work, t);
-  work(0);
-  for (auto& x : th) x.join();
+  parallel_for_fn(n, threads, std::function<void(uint64_t)>(fn));
 }
+
+}  // namespace cpu
+}  // namespace nt

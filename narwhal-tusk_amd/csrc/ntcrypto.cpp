@@ -91,6 +91,8 @@ enum { B_DATA, B_OFF, B_LEN, B_PK, B_SIG, B_OUT, B_OUT2, B_FIRST, B_CNT, B_STASH
 
 struct Device {
   int ordinal = -1;
+  int group = -1;               // index of this device entry in nt_ctx::devs (keyset tables)
+  bool owns_comb = true;        // false for the extra slots (they share the entry's comb of B)
   hipStream_t stream = nullptr;
   uint32_t* d_combB = nullptr;  // wide comb of B (verify, key-cache verify, sign)
   void* d_ws = nullptr;
@@ -112,6 +114,13 @@ struct Device {
   std::mutex mu;
   DevBuf d[B_NBUF];
   HostBuf h[B_NBUF];
+  // Extra execution slots of the same device entry (NT_SLOTS, default 2 in
+  // all): each has its own streams, workspace and staging and shares the comb
+  // of B, so a long call (a batch of digests) on one slot does not block a
+  // concurrent call (a certificate batch) on the device -- both run on the GPU
+  // at once.  Host entry points take the first free slot (SURVEY §8(b):
+  // "per-call stream acquisition from a pool").
+  std::vector<std::unique_ptr<Device>> extra;
 
   ~Device() {
     if (ordinal < 0) return;
@@ -121,7 +130,9 @@ struct Device {
       if (b.p) (void)hipFree(b.p);
     for (auto& b : h)
       if (b.p) (void)hipHostFree(b.p);
-    if (d_combB) (void)hipFree(d_combB);
+    extra.clear();  // before this entry's comb, which the extra slots borrow
+    (void)hipSetDevice(ordinal);
+    if (d_combB && owns_comb) (void)hipFree(d_combB);
     if (d_ws) (void)hipFree(d_ws);
     if (ws_done) (void)hipEventDestroy(ws_done);
     if (stash_done) (void)hipEventDestroy(stash_done);
@@ -137,8 +148,9 @@ struct Device {
     if (stream) (void)hipStreamDestroy(stream);
   }
 
-  int init(int ord) {
+  int init(int ord, int grp, const Device* share = nullptr) {
     ordinal = ord;
+    group = grp;
     NT_TRY(hipSetDevice(ord));
     hipDeviceProp_t prop;
     NT_TRY(hipGetDeviceProperties(&prop, ord));
@@ -151,7 +163,10 @@ struct Device {
     NT_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
     NT_TRY(hipEventCreateWithFlags(&join2, hipEventDisableTiming));
     NT_TRY(hipEventCreateWithFlags(&ws2_done, hipEventDisableTiming));
-    {
+    if (share) {
+      d_combB = share->d_combB;
+      owns_comb = false;
+    } else {
       static const uint32_t kB[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                                      0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
       if (hipMalloc(&d_combB, nt::wcomb_bytes_per_key(nt::bcomb_bits())) != hipSuccess) return NT_ENOMEM;
@@ -303,14 +318,26 @@ const char* nt_strerror(int code) {
 
 const char* nt_version(void) { return "ntcrypto 0.1 gfx950"; }
 
+static long env_slots() {
+  const char* e = std::getenv("NT_SLOTS");
+  return e && *e ? std::atol(e) : 2;
+}
+
 static int init_common(nt_ctx** out, const std::vector<int>& ords) {
   if (!out) return NT_EINVAL;
   *out = nullptr;
   auto ctx = std::make_unique<nt_ctx>();
+  const int slots = std::max(1, std::min(8, (int)env_slots()));
   for (int o : ords) {
     auto d = std::make_unique<Device>();
-    const int rc = d->init(o);
+    int rc = d->init(o, (int)ctx->devs.size());
     if (rc != NT_OK) return rc;
+    for (int k = 1; k < slots; ++k) {
+      auto x = std::make_unique<Device>();
+      rc = x->init(o, (int)ctx->devs.size(), d.get());
+      if (rc != NT_OK) return rc;
+      d->extra.push_back(std::move(x));
+    }
     ctx->devs.push_back(std::move(d));
   }
   if (ctx->devs.empty()) return NT_ENODEV;
@@ -400,13 +427,33 @@ std::vector<std::pair<uint64_t, uint64_t>> shard(uint64_t n, size_t ndev, uint64
   return r;
 }
 
+// A free execution slot of device entry d (its own or an extra one), locked
+// into lk; when every slot is busy, wait for the entry's first slot.
+Device& acquire_slot(nt_ctx* ctx, size_t d, std::unique_lock<std::mutex>& lk) {
+  Device& p = *ctx->devs[d];
+  std::unique_lock<std::mutex> l0(p.mu, std::try_to_lock);
+  if (l0.owns_lock()) {
+    lk = std::move(l0);
+    return p;
+  }
+  for (auto& x : p.extra) {
+    std::unique_lock<std::mutex> l(x->mu, std::try_to_lock);
+    if (l.owns_lock()) {
+      lk = std::move(l);
+      return *x;
+    }
+  }
+  lk = std::unique_lock<std::mutex>(p.mu);
+  return p;
+}
+
 template <class F>
 int run_sharded(nt_ctx* ctx, uint64_t n, uint64_t align, F&& fn) {
   const size_t nd = ctx->devs.size();
   auto parts = shard(n, nd, align);
   if (nd == 1) {
-    Device& dv = *ctx->devs[0];
-    std::lock_guard<std::mutex> lk(dv.mu);
+    std::unique_lock<std::mutex> lk;
+    Device& dv = acquire_slot(ctx, 0, lk);
     if (hipSetDevice(dv.ordinal) != hipSuccess) return NT_EHIP;
     return fn(dv, parts[0].first, parts[0].second);
   }
@@ -415,8 +462,8 @@ int run_sharded(nt_ctx* ctx, uint64_t n, uint64_t align, F&& fn) {
   for (size_t d = 0; d < nd; ++d) {
     if (parts[d].first >= parts[d].second) continue;
     th.emplace_back([&, d] {
-      Device& dv = *ctx->devs[d];
-      std::lock_guard<std::mutex> lk(dv.mu);
+      std::unique_lock<std::mutex> lk;
+      Device& dv = acquire_slot(ctx, d, lk);
       if (hipSetDevice(dv.ordinal) != hipSuccess) {
         rcs[d] = NT_EHIP;
         return;
@@ -632,7 +679,9 @@ Device* dev_of(nt_ctx* ctx, int dev) {
 
 // ---- small-call path (cpu_lane.hpp) -----------------------------
 // Cost model of one host entry-point call, from the `latency` block of
-// bench.py on MI355X (profiles/r02/latency_*.json).  A GPU call below one
+// bench.py on MI355X + EPYC 9575F (profiles/r02/bench_latency_v1.json: host lane
+// 31-35 us per verify and 884 MB/s of SHA-512 per thread; a GPU verify call
+// below one round 1.33 ms, a lone 508,052-B digest 16.9 ms).  A GPU call below one
 // round of resident waves costs a fixed floor (launch + copies + the two
 // signatures every lane of the verify kernel runs); the digest kernel's time
 // is set by its LONGEST message (one lane's serial chain) plus the PCIe copy.
@@ -644,13 +693,13 @@ double env_or(const char* name, double dflt) {
 struct SmallModel {
   double cpu_verify_us, gpu_verify_us, cpu_sha_mbs, gpu_lane_mbs, gpu_call_us, pcie_gbs, spawn_us;
   SmallModel()
-      : cpu_verify_us(env_or("NT_SMALL_CPU_VERIFY_US", 75.0)),
-        gpu_verify_us(env_or("NT_SMALL_GPU_VERIFY_US", 1700.0)),
-        cpu_sha_mbs(env_or("NT_SMALL_CPU_SHA_MBS", 450.0)),
+      : cpu_verify_us(env_or("NT_SMALL_CPU_VERIFY_US", 36.0)),
+        gpu_verify_us(env_or("NT_SMALL_GPU_VERIFY_US", 1300.0)),
+        cpu_sha_mbs(env_or("NT_SMALL_CPU_SHA_MBS", 850.0)),
         gpu_lane_mbs(env_or("NT_SMALL_GPU_LANE_MBS", 30.0)),
         gpu_call_us(env_or("NT_SMALL_GPU_CALL_US", 60.0)),
         pcie_gbs(env_or("NT_SMALL_PCIE_GBS", 20.0)),
-        spawn_us(env_or("NT_SMALL_SPAWN_US", 40.0)) {}
+        spawn_us(env_or("NT_SMALL_SPAWN_US", 15.0)) {}
 };
 const SmallModel& small_model() {
   static const SmallModel m;
@@ -857,11 +906,7 @@ static void stage_groups(uint64_t glo, uint64_t ghi, const uint64_t* first, cons
 
 namespace {
 
-int dev_index(nt_ctx* ctx, const Device& dv) {
-  for (size_t i = 0; i < ctx->devs.size(); ++i)
-    if (ctx->devs[i].get() == &dv) return (int)i;
-  return -1;
-}
+int dev_index(nt_ctx*, const Device& dv) { return dv.group; }
 
 // Certificate groups through either key form: ks == nullptr -> kw = 32-byte
 // encodings (verify kernel, cofactorless), else kw = 4-byte committee indices

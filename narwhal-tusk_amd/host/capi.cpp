@@ -2,10 +2,13 @@
 // (ctypes): the wire codec (CPU only) and the batched primary::Core ingestion
 // path of SURVEY §8(f).1/(f).2 (GPU through libntcrypto).  Not part of the
 // crypto crate's boundary (include/ntcrypto.h is).
+#include <algorithm>
 #include <cstring>
+#include <future>
 #include <exception>
 #include <memory>
 
+#include "../../include/ntcrypto.h"
 #include "narwhal.hpp"
 #include "wire.hpp"
 
@@ -116,6 +119,68 @@ void ntn_last_ingest_stats(double out[6]) {
   out[3] = s.strict;
   out[4] = s.batch;
   out[5] = s.total;
+}
+
+// ---- worker::DigestBatcher -------------------------------
+void* ntn_batcher_new(uint64_t max_bytes, uint64_t max_batches, uint32_t max_delay_us) {
+  try {
+    worker::DigestBatcher::Policy p;
+    p.max_bytes = (size_t)max_bytes;
+    p.max_batches = (size_t)max_batches;
+    p.max_delay_us = max_delay_us;
+    return new worker::DigestBatcher(p);
+  } catch (const std::exception&) {
+    return nullptr;
+  }
+}
+void ntn_batcher_free(void* b) { delete (worker::DigestBatcher*)b; }
+
+// queue one serialized batch of Processor (worker_id, own); returns a ticket
+// for ntn_batcher_wait (NULL on failure)
+void* ntn_batcher_submit(void* b, uint32_t worker_id, int own, const uint8_t* data, uint64_t len) {
+  try {
+    worker::Processor p{worker_id, own != 0};
+    return new std::future<worker::DigestBatcher::Output>(
+        ((worker::DigestBatcher*)b)->submit(p, data, (size_t)len));
+  } catch (const std::exception&) {
+    return nullptr;
+  }
+}
+
+// wait for a ticket (and free it): digest32 (32 bytes) and the Processor's
+// 40-byte output message; 0, or -2 if the backend failed
+int ntn_batcher_wait(void* ticket, uint8_t* digest32, uint8_t* msg40) {
+  auto* f = (std::future<worker::DigestBatcher::Output>*)ticket;
+  int rc = 0;
+  try {
+    const auto o = f->get();
+    std::memcpy(digest32, o.digest.bytes.data(), 32);
+    std::memcpy(msg40, o.message.data(), std::min<size_t>(40, o.message.size()));
+  } catch (const std::exception&) {
+    rc = -2;
+  }
+  delete f;
+  return rc;
+}
+
+void ntn_batcher_flush(void* b) { ((worker::DigestBatcher*)b)->flush(); }
+
+// flushes, batches, bytes, seconds inside nt_sha512_trunc32
+void ntn_batcher_stats(void* b, double out[4]) {
+  const auto s = ((worker::DigestBatcher*)b)->stats();
+  out[0] = (double)s.flushes;
+  out[1] = (double)s.batches;
+  out[2] = (double)s.bytes;
+  out[3] = s.hash_seconds;
+}
+
+// the small-call path of the mirror's shared context (include/ntcrypto.h)
+int ntn_set_small_call_path(int mode, int threads) {
+  try {
+    return nt_set_small_call_path(crypto::Backend::global().ctx(), mode, threads);
+  } catch (const std::exception&) {
+    return -2;
+  }
 }
 
 }  // extern "C"

@@ -1,10 +1,12 @@
 // narwhal.cpp -- primary/worker caller mirrors over the crypto mirror.
 #include "narwhal.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <thread>
 
+#include "../../include/ntcrypto.h"
 #include "wire.hpp"
 
 namespace primary {
@@ -362,29 +364,153 @@ std::vector<DagError> Core::ingest_general(const uint8_t* data, const uint64_t* 
 
 namespace worker {
 
-size_t DigestBatcher::submit(const Processor& p, std::vector<uint8_t> serialized_batch) {
-  procs_.push_back(p);
-  batches_.push_back(std::move(serialized_batch));
-  return batches_.size() - 1;
+namespace {
+// processor.rs:40-48: bincode WorkerPrimaryMessage::{OurBatch, OthersBatch}(digest, worker id)
+std::vector<uint8_t> processor_message(const Processor& p, const crypto::Digest& d) {
+  std::vector<uint8_t> msg;
+  const uint32_t tag = p.own_digest ? 0 : 1;
+  for (int i = 0; i < 4; ++i) msg.push_back((uint8_t)(tag >> (8 * i)));
+  msg.insert(msg.end(), d.bytes.begin(), d.bytes.end());
+  for (int i = 0; i < 4; ++i) msg.push_back((uint8_t)(p.id >> (8 * i)));
+  return msg;
+}
+}  // namespace
+
+// One side of the double buffer: the batches' bytes back to back in pinned
+// memory (nt_host_alloc), their offsets / lengths, and the waiting Processors.
+struct DigestBatcher::Queue {
+  uint8_t* arena = nullptr;
+  size_t cap = 0, used = 0;
+  std::vector<uint64_t> off, len;
+  std::vector<Processor> procs;
+  std::vector<std::promise<Output>> waiters;
+  std::chrono::steady_clock::time_point oldest;
+  ~Queue() {
+    if (arena) nt_host_free(arena);
+  }
+  void reserve(size_t need) {
+    if (need <= cap) return;
+    size_t c = std::max<size_t>(need, std::max<size_t>(2 * cap, 1u << 20));
+    auto* a = (uint8_t*)nt_host_alloc(c);
+    if (!a) throw crypto::BackendError("nt_host_alloc failed");
+    if (used) std::memcpy(a, arena, used);
+    if (arena) nt_host_free(arena);
+    arena = a;
+    cap = c;
+  }
+  void clear() {
+    used = 0;
+    off.clear();
+    len.clear();
+    procs.clear();
+    waiters.clear();
+  }
+};
+
+DigestBatcher::DigestBatcher() : DigestBatcher(Policy()) {}
+
+DigestBatcher::DigestBatcher(Policy policy)
+    : policy_(policy), front_(std::make_unique<Queue>()), back_(std::make_unique<Queue>()) {
+  th_ = std::thread([this] { run(); });
 }
 
-std::vector<std::vector<uint8_t>> DigestBatcher::flush(std::vector<crypto::Digest>* digests) {
-  const auto dig = batch_digests(batches_);  // one SHA-512 launch for both streams
-  std::vector<std::vector<uint8_t>> out;
-  out.reserve(dig.size());
-  for (size_t i = 0; i < dig.size(); ++i) {
-    // the Processor's output message (processor.rs:40-48) around the batched digest
-    std::vector<uint8_t> msg;
-    const uint32_t tag = procs_[i].own_digest ? 0 : 1;
-    for (int b = 0; b < 4; ++b) msg.push_back((uint8_t)(tag >> (8 * b)));
-    msg.insert(msg.end(), dig[i].bytes.begin(), dig[i].bytes.end());
-    for (int b = 0; b < 4; ++b) msg.push_back((uint8_t)(procs_[i].id >> (8 * b)));
-    out.push_back(std::move(msg));
+DigestBatcher::~DigestBatcher() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
   }
-  if (digests) *digests = dig;
-  procs_.clear();
-  batches_.clear();
-  return out;
+  cv_.notify_all();
+  th_.join();
+}
+
+std::future<DigestBatcher::Output> DigestBatcher::submit(const Processor& p, const uint8_t* data, size_t len) {
+  std::promise<Output> pr;
+  auto fut = pr.get_future();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    Queue& q = *front_;
+    if (q.off.empty()) q.oldest = std::chrono::steady_clock::now();
+    q.reserve(q.used + len + 1);
+    if (len) std::memcpy(q.arena + q.used, data, len);
+    q.off.push_back(q.used);
+    q.len.push_back(len);
+    q.used += len;
+    q.procs.push_back(p);
+    q.waiters.push_back(std::move(pr));
+  }
+  cv_.notify_all();
+  return fut;
+}
+
+void DigestBatcher::flush() {
+  std::unique_lock<std::mutex> lk(mu_);
+  const uint64_t ticket = ++flush_req_;
+  force_ = true;
+  cv_.notify_all();
+  done_cv_.wait(lk, [&] { return flush_done_ >= ticket; });
+}
+
+size_t DigestBatcher::pending() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return front_->off.size();
+}
+
+DigestBatcher::Stats DigestBatcher::stats() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return stats_;
+}
+
+// Flusher: wait until a flush rule fires (bytes, batch count, age of the
+// oldest batch, an explicit flush or shutdown), swap the queues, hash the
+// taken queue with one C-ABI call while submitters fill the other one.
+void DigestBatcher::run() {
+  std::unique_lock<std::mutex> lk(mu_);
+  for (;;) {
+    auto due = [&] {
+      const Queue& q = *front_;
+      return stop_ || force_ || q.used >= policy_.max_bytes || q.off.size() >= policy_.max_batches;
+    };
+    if (front_->off.empty()) {
+      cv_.wait(lk, [&] { return stop_ || force_ || !front_->off.empty(); });
+    } else if (!due()) {
+      cv_.wait_until(lk, front_->oldest + std::chrono::microseconds(policy_.max_delay_us), due);
+    }
+    const bool stopping = stop_;
+    const uint64_t req = flush_req_;  // every flush() so far is served by this swap
+    force_ = false;
+    std::swap(front_, back_);
+    lk.unlock();
+    if (!back_->off.empty()) hash(*back_);
+    back_->clear();
+    lk.lock();
+    flush_done_ = std::max(flush_done_, req);
+    done_cv_.notify_all();
+    if (stopping && front_->off.empty()) return;
+  }
+}
+
+void DigestBatcher::hash(Queue& q) {
+  const size_t n = q.off.size();
+  std::vector<crypto::Digest> dig(n);
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = nt_sha512_trunc32(crypto::Backend::global().ctx(), q.arena, q.off.data(), q.len.data(), n,
+                                   dig[0].bytes.data());
+  const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.flushes += 1;
+    stats_.batches += n;
+    stats_.bytes += q.used;
+    stats_.hash_seconds += dt;
+  }
+  for (size_t i = 0; i < n; ++i) {
+    if (rc != NT_OK) {  // a backend failure is an error for every waiter, never a digest
+      q.waiters[i].set_exception(std::make_exception_ptr(
+          crypto::BackendError(std::string("nt_sha512_trunc32 failed: ") + nt_strerror(rc))));
+      continue;
+    }
+    q.waiters[i].set_value(Output{dig[i], processor_message(q.procs[i], dig[i])});
+  }
 }
 
 std::vector<uint8_t> serialize_batch(const Batch& batch) {
@@ -409,12 +535,7 @@ std::vector<crypto::Digest> batch_digests(const std::vector<std::vector<uint8_t>
 std::vector<uint8_t> Processor::process(const std::vector<uint8_t>& serialized_batch, crypto::Digest* digest_out) const {
   const crypto::Digest d = batch_digest(serialized_batch);
   if (digest_out) *digest_out = d;
-  std::vector<uint8_t> msg;
-  const uint32_t tag = own_digest ? 0 : 1;  // OurBatch / OthersBatch
-  for (int i = 0; i < 4; ++i) msg.push_back((uint8_t)(tag >> (8 * i)));
-  msg.insert(msg.end(), d.bytes.begin(), d.bytes.end());
-  for (int i = 0; i < 4; ++i) msg.push_back((uint8_t)(id >> (8 * i)));
-  return msg;
+  return processor_message(*this, d);
 }
 
 }  // namespace worker

@@ -14,8 +14,12 @@
 //                                           worker/src/batch_maker.rs:117-119,
 //                                           worker/src/processor.rs:35-55 (§8(f).3)
 #pragma once
+#include <condition_variable>
 #include <cstdint>
+#include <future>
 #include <map>
+#include <mutex>
+#include <thread>
 #include <memory>
 #include <optional>
 #include <set>
@@ -176,21 +180,62 @@ struct Processor {
   std::vector<uint8_t> process(const std::vector<uint8_t>& serialized_batch, crypto::Digest* digest_out = nullptr) const;
 };
 
-// Worker digest batching: the two Processor tasks of a worker
-// (worker.rs:182-188 own batches, :227-233 others' batches) feed one batcher;
-// every flush hashes all queued batches in ONE SHA-512 launch and returns each
-// Processor's output message in submission order.
+// Worker digest batching.  The two Processor tasks of a
+// worker (worker.rs:182-188 own batches, :227-233 others' batches) submit into
+// one batcher from their own threads; a flusher thread hashes everything queued
+// in ONE nt_sha512_trunc32 call when the queued bytes reach max_bytes, the
+// queue reaches max_batches, or the oldest queued batch is max_delay_us old.
+// submit() copies the batch once into a pinned arena (so the call DMAs it
+// without a staging copy) and returns a future of the Processor's output
+// (processor.rs:38-48: the digest and the bincode WorkerPrimaryMessage).  A
+// Processor that keeps several batches in flight awaits its futures in
+// submission order, so its outputs keep the reference's order.  Whether a flush
+// runs on the GPU or on the host lane is the C ABI's small-call decision
+// (nt_set_small_call_path on the shared context).
 class DigestBatcher {
  public:
-  // queue one serialized batch for Processor p; returns its ticket
-  size_t submit(const Processor& p, std::vector<uint8_t> serialized_batch);
-  // hash everything queued (one launch) -> (ticket order) Processor::process outputs
-  std::vector<std::vector<uint8_t>> flush(std::vector<crypto::Digest>* digests = nullptr);
-  size_t pending() const { return batches_.size(); }
+  struct Policy {
+    size_t max_bytes = 256u << 20;
+    size_t max_batches = 4096;
+    uint32_t max_delay_us = 1000;
+  };
+  struct Output {
+    crypto::Digest digest;
+    std::vector<uint8_t> message;  // bincode WorkerPrimaryMessage::{OurBatch, OthersBatch}(digest, id)
+  };
+  struct Stats {
+    uint64_t flushes = 0, batches = 0, bytes = 0;
+    double hash_seconds = 0;  // inside nt_sha512_trunc32
+  };
+  DigestBatcher();
+  explicit DigestBatcher(Policy policy);
+  ~DigestBatcher();  // hashes what is still queued, then stops the flusher
+  DigestBatcher(const DigestBatcher&) = delete;
+  DigestBatcher& operator=(const DigestBatcher&) = delete;
+
+  std::future<Output> submit(const Processor& p, const uint8_t* data, size_t len);
+  std::future<Output> submit(const Processor& p, const std::vector<uint8_t>& serialized) {
+    return submit(p, serialized.data(), serialized.size());
+  }
+  // Processor::process through the batcher: submit and wait
+  Output process(const Processor& p, const std::vector<uint8_t>& serialized) { return submit(p, serialized).get(); }
+  void flush();  // hash everything queued now
+  size_t pending() const;
+  Stats stats() const;
 
  private:
-  std::vector<Processor> procs_;
-  std::vector<std::vector<uint8_t>> batches_;
+  struct Queue;
+  void run();
+  void hash(Queue& q);
+  Policy policy_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::unique_ptr<Queue> front_, back_;  // submit into front_, the flusher hashes back_
+  bool stop_ = false, force_ = false;
+  uint64_t flush_req_ = 0, flush_done_ = 0;
+  std::condition_variable done_cv_;
+  Stats stats_;
+  std::thread th_;
 };
 
 }  // namespace worker

@@ -49,6 +49,20 @@ def load():
         lib.ntn_core_ingest_pipelined.restype = ctypes.c_int
         lib.ntn_last_ingest_stats.argtypes = [ctypes.POINTER(ctypes.c_double)]
         lib.ntn_last_ingest_stats.restype = None
+        lib.ntn_batcher_new.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
+        lib.ntn_batcher_new.restype = ctypes.c_void_p
+        lib.ntn_batcher_free.argtypes = [ctypes.c_void_p]
+        lib.ntn_batcher_free.restype = None
+        lib.ntn_batcher_submit.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, _u8p, ctypes.c_uint64]
+        lib.ntn_batcher_submit.restype = ctypes.c_void_p
+        lib.ntn_batcher_wait.argtypes = [ctypes.c_void_p, _u8p, _u8p]
+        lib.ntn_batcher_wait.restype = ctypes.c_int
+        lib.ntn_batcher_flush.argtypes = [ctypes.c_void_p]
+        lib.ntn_batcher_flush.restype = None
+        lib.ntn_batcher_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
+        lib.ntn_batcher_stats.restype = None
+        lib.ntn_set_small_call_path.argtypes = [ctypes.c_int, ctypes.c_int]
+        lib.ntn_set_small_call_path.restype = ctypes.c_int
         _lib = lib
     return _lib
 
@@ -142,6 +156,67 @@ class Core:
     def close(self):
         if self._h:
             load().ntn_core_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def set_small_call_path(mode, threads=0):
+    """The small-call path of the mirror's shared context (nt_set_small_call_path)."""
+    rc = load().ntn_set_small_call_path(int(mode), int(threads))
+    if rc != 0:
+        raise NtError("ntn_set_small_call_path failed (%d)" % rc)
+
+
+class DigestBatcher:
+    """worker::DigestBatcher (SURVEY §8(f).3; host/narwhal.hpp): both Processor
+    tasks of a worker submit serialized batches from their own threads; a
+    flusher hashes everything queued in one nt_sha512_trunc32 call when
+    max_bytes / max_batches is reached or the oldest batch is max_delay_us old.
+
+    submit() returns a ticket; wait(ticket) -> (digest32 bytes, 40-byte
+    WorkerPrimaryMessage).  ctypes releases the GIL in both, so Python threads
+    submit and wait concurrently."""
+
+    def __init__(self, max_bytes=256 << 20, max_batches=4096, max_delay_us=1000):
+        self._lib = load()
+        self._h = self._lib.ntn_batcher_new(max_bytes, max_batches, max_delay_us)
+        if not self._h:
+            raise NtError("ntn_batcher_new failed")
+
+    def submit(self, worker_id, own, batch):
+        a, p = _buf(batch)
+        t = self._lib.ntn_batcher_submit(self._h, worker_id, 1 if own else 0, p, len(batch))
+        if not t:
+            raise NtError("ntn_batcher_submit failed")
+        return t
+
+    def wait(self, ticket):
+        d = np.zeros(32, np.uint8)
+        m = np.zeros(40, np.uint8)
+        rc = self._lib.ntn_batcher_wait(ticket, d.ctypes.data_as(_u8p), m.ctypes.data_as(_u8p))
+        if rc != 0:
+            raise NtError("digest batcher: backend failure")
+        return d.tobytes(), m.tobytes()
+
+    def process(self, worker_id, own, batch):
+        return self.wait(self.submit(worker_id, own, batch))
+
+    def flush(self):
+        self._lib.ntn_batcher_flush(self._h)
+
+    def stats(self):
+        out = (ctypes.c_double * 4)()
+        self._lib.ntn_batcher_stats(self._h, out)
+        return {"flushes": int(out[0]), "batches": int(out[1]), "bytes": int(out[2]), "hash_seconds": out[3]}
+
+    def close(self):
+        if self._h:
+            self._lib.ntn_batcher_free(self._h)
             self._h = None
 
     def __del__(self):
