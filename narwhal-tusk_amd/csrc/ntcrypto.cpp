@@ -138,13 +138,13 @@ struct Device {
     if (stash_done) (void)hipEventDestroy(stash_done);
     for (auto& e : cev)
       if (e) (void)hipEventDestroy(e);
-    if (stream2) (void)hipStreamSynchronize(stream2);
+    if (stream2 && stream2 != stream) (void)hipStreamSynchronize(stream2);
     if (ws2.p) (void)hipFree(ws2.p);
     if (stash2.p) (void)hipFree(stash2.p);
     if (join2) (void)hipEventDestroy(join2);
     if (ws2_done) (void)hipEventDestroy(ws2_done);
-    if (stream2) (void)hipStreamDestroy(stream2);
-    if (cstream) (void)hipStreamDestroy(cstream);
+    if (stream2 && stream2 != stream) (void)hipStreamDestroy(stream2);
+    if (cstream && cstream != stream) (void)hipStreamDestroy(cstream);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -155,12 +155,24 @@ struct Device {
     hipDeviceProp_t prop;
     NT_TRY(hipGetDeviceProperties(&prop, ord));
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NT_ENODEV;
-    NT_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    if (share) {
+      // an extra (latency) slot: ONE stream at the highest priority for its
+      // copies and kernels, so it does not share a hardware queue with the
+      // bulk streams of the entry's first slot (HIP multiplexes a process's
+      // streams over GPU_MAX_HW_QUEUES = 4 queues; a kernel behind a 17 ms
+      // digest flush in the same queue waits for it)
+      int lo = 0, hi = 0;
+      NT_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      NT_TRY(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
+      cstream = stream2 = stream;
+    } else {
+      NT_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+      NT_TRY(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+      NT_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+    }
     NT_TRY(hipEventCreateWithFlags(&ws_done, hipEventDisableTiming));
     NT_TRY(hipEventCreateWithFlags(&stash_done, hipEventDisableTiming));
-    NT_TRY(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
     for (auto& e : cev) NT_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    NT_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
     NT_TRY(hipEventCreateWithFlags(&join2, hipEventDisableTiming));
     NT_TRY(hipEventCreateWithFlags(&ws2_done, hipEventDisableTiming));
     if (share) {
@@ -427,33 +439,47 @@ std::vector<std::pair<uint64_t, uint64_t>> shard(uint64_t n, size_t ndev, uint64
   return r;
 }
 
-// A free execution slot of device entry d (its own or an extra one), locked
-// into lk; when every slot is busy, wait for the entry's first slot.
-Device& acquire_slot(nt_ctx* ctx, size_t d, std::unique_lock<std::mutex>& lk) {
+// A free execution slot of device entry d, locked into lk.  Latency-sized
+// calls try the extra (high-priority) slots first, bulk calls the entry's own
+// slot first; when every slot is busy, wait for the preferred one.
+Device& acquire_slot(nt_ctx* ctx, size_t d, bool latency, std::unique_lock<std::mutex>& lk) {
   Device& p = *ctx->devs[d];
-  std::unique_lock<std::mutex> l0(p.mu, std::try_to_lock);
-  if (l0.owns_lock()) {
-    lk = std::move(l0);
-    return p;
-  }
-  for (auto& x : p.extra) {
-    std::unique_lock<std::mutex> l(x->mu, std::try_to_lock);
+  std::vector<Device*> order;
+  if (!latency) order.push_back(&p);
+  for (auto& x : p.extra) order.push_back(x.get());
+  if (latency) order.push_back(&p);
+  for (Device* s : order) {
+    std::unique_lock<std::mutex> l(s->mu, std::try_to_lock);
     if (l.owns_lock()) {
       lk = std::move(l);
-      return *x;
+      return *s;
     }
   }
-  lk = std::unique_lock<std::mutex>(p.mu);
-  return p;
+  lk = std::unique_lock<std::mutex>(order[0]->mu);
+  return *order[0];
+}
+
+// digests whose longest message is short (header / vote / certificate
+// preimages) finish fast; long ones (worker batches) are bulk
+bool sha_latency(uint64_t n, const uint64_t* len) {
+  for (uint64_t i = 0; i < n; ++i)
+    if (len[i] > (64u << 10)) return false;
+  return true;
+}
+
+// work below one round of resident waves: a latency-sized call
+bool latency_sized(const nt_ctx* ctx, uint64_t items_per_device, uint64_t round) {
+  (void)ctx;
+  return items_per_device <= round;
 }
 
 template <class F>
-int run_sharded(nt_ctx* ctx, uint64_t n, uint64_t align, F&& fn) {
+int run_sharded(nt_ctx* ctx, uint64_t n, uint64_t align, F&& fn, bool latency = false) {
   const size_t nd = ctx->devs.size();
   auto parts = shard(n, nd, align);
   if (nd == 1) {
     std::unique_lock<std::mutex> lk;
-    Device& dv = acquire_slot(ctx, 0, lk);
+    Device& dv = acquire_slot(ctx, 0, latency, lk);
     if (hipSetDevice(dv.ordinal) != hipSuccess) return NT_EHIP;
     return fn(dv, parts[0].first, parts[0].second);
   }
@@ -463,7 +489,7 @@ int run_sharded(nt_ctx* ctx, uint64_t n, uint64_t align, F&& fn) {
     if (parts[d].first >= parts[d].second) continue;
     th.emplace_back([&, d] {
       std::unique_lock<std::mutex> lk;
-      Device& dv = acquire_slot(ctx, d, lk);
+      Device& dv = acquire_slot(ctx, d, latency, lk);
       if (hipSetDevice(dv.ordinal) != hipSuccess) {
         rcs[d] = NT_EHIP;
         return;
@@ -815,7 +841,7 @@ int nt_sha512_trunc32(nt_ctx* ctx, const uint8_t* data, const uint64_t* off, con
     NT_TRY(hipMemcpyAsync(out32 + 32 * lo, dv.d[B_OUT].p, m * 32, hipMemcpyDeviceToHost, dv.stream));
     NT_TRY(hipStreamSynchronize(dv.stream));
     return NT_OK;
-  });
+  }, sha_latency(n, len));
 }
 
 int nt_ed25519_verify_strict(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* sig64,
@@ -860,7 +886,7 @@ int nt_ed25519_verify_strict(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* si
     NT_TRY(hipStreamSynchronize(dv.stream));
     words_to_bitmap(out_bitmap + lo / 8, dv.h[B_OUT].as<uint64_t>(), m);
     return NT_OK;
-  });
+  }, latency_sized(ctx, (n + ctx->devs.size() - 1) / ctx->devs.size(), nt::verify_round_sigs(ctx->devs[0]->cus)));
 }
 
 // Stage certificate groups [glo, ghi) contiguously into pinned host buffers:
@@ -1032,7 +1058,7 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
       }
     }
     return NT_OK;
-  });
+  }, latency_sized(ctx, (nsig_total + ctx->devs.size() - 1) / ctx->devs.size(), ks ? nt::keyset_round_sigs(ctx->devs[0]->cus) : nt::verify_round_sigs(ctx->devs[0]->cus)));
 }
 
 }  // namespace
@@ -1235,7 +1261,7 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
     NT_TRY(hipStreamSynchronize(dv.stream));
     words_to_bitmap(out_bitmap + lo / 8, dv.h[B_OUT].as<uint64_t>(), m);
     return NT_OK;
-  });
+  }, latency_sized(ctx, (n + ctx->devs.size() - 1) / ctx->devs.size(), nt::keyset_round_sigs(ctx->devs[0]->cus)));
 }
 
 int nt_ed25519_verify_batch_groups_keyset(nt_ctx* ctx, const nt_keyset* ks, const uint32_t* key_idx,

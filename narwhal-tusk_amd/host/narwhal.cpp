@@ -470,11 +470,12 @@ void DigestBatcher::run() {
       const Queue& q = *front_;
       return stop_ || force_ || q.used >= policy_.max_bytes || q.off.size() >= policy_.max_batches;
     };
-    if (front_->off.empty()) {
+    if (!stop_ && !force_ && front_->off.empty()) {
       cv_.wait(lk, [&] { return stop_ || force_ || !front_->off.empty(); });
-    } else if (!due()) {
-      cv_.wait_until(lk, front_->oldest + std::chrono::microseconds(policy_.max_delay_us), due);
+      continue;  // the first batch starts the age clock: re-evaluate the rules
     }
+    // returns when a rule fires or at the oldest batch's deadline (age rule)
+    if (!due()) cv_.wait_until(lk, front_->oldest + std::chrono::microseconds(policy_.max_delay_us), due);
     const bool stopping = stop_;
     const uint64_t req = flush_req_;  // every flush() so far is served by this swap
     force_ = false;

@@ -66,15 +66,21 @@ def test_two_processors_real_batches(small):
 def test_flush_rules():
     N.set_small_call_path(0)
     xs = [bytes([i]) * (1000 + i) for i in range(12)]
-    # batch-count rule: at most 4 per flush
+    # batch-count rule: the 4th queued batch triggers a flush (the age rule
+    # would take 10 s)
     b = N.DigestBatcher(max_bytes=1 << 30, max_batches=4, max_delay_us=10_000_000)
     try:
-        tickets = [b.submit(0, True, x) for x in xs]
-        b.flush()  # the remainder
+        t0 = time.perf_counter()
+        tickets = [b.submit(0, True, x) for x in xs[:4]]
         for x, t in zip(xs, tickets):
             assert b.wait(t)[0] == hashlib.sha512(x).digest()[:32]
-        st = b.stats()
-        assert st["batches"] == 12 and st["flushes"] >= 3
+        assert time.perf_counter() - t0 < 5.0
+        # explicit flush of a partial queue
+        tickets = [b.submit(0, True, x) for x in xs[4:6]]
+        b.flush()
+        assert [b.wait(t)[0] for t in tickets] == [hashlib.sha512(x).digest()[:32] for x in xs[4:6]]
+        assert time.perf_counter() - t0 < 5.0
+        assert b.stats()["batches"] == 6
     finally:
         b.close()
     # age rule: a lone batch is hashed after max_delay_us without any flush()
