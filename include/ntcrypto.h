@@ -27,8 +27,12 @@
  *   - Return 0 on success, < 0 on failure (NT_E*).  A caller must never turn a
  *     negative return into "reject"; there is NO CPU fallback inside this
  *     library: without a usable gfx950 device nt_init fails with NT_ENODEV.
- *   - Thread-safe: calls on one context may come from several threads; work
- *     on each device is serialized by a per-device lock.
+ *   - Thread-safe: calls on one context may come from several threads.  Each
+ *     device entry has NT_SLOTS (default 2) execution slots -- own streams,
+ *     workspace and staging -- and a call takes a free one, so a long call (a
+ *     batch of digests) does not block a concurrent short one (a certificate
+ *     batch): small calls prefer the extra slot, whose single stream has the
+ *     highest priority; bulk calls the entry's own slot.
  *   - Multi-GPU: host entry points shard items by contiguous index ranges
  *     over the context's devices (certificates are never split); no
  *     collective, results gathered on the host.
@@ -112,7 +116,8 @@ int nt_ed25519_keypair_batch(nt_ctx *ctx, const uint8_t *seed32, uint64_t n, uin
  * (the wide comb of -A: 20-bit digits, 13 x 524289 affine niels entries =
  * 872 MB per key when every device can hold them with 1/8 of its HBM to
  * spare -- 87 GB for n = 100 -- else 16-bit digits, 16 x 32769 entries =
- * 67 MB per key; NT_KEYSET_COMB_BITS=16|20 forces one) plus each key's raw
+ * 67 MB per key; NT_KEYSET_COMB_BITS=16|18|20 forces one -- 18 bits: 15 x
+ * 131073 entries = 252 MB per key) plus each key's raw
  * encoding and decode / small-order flags, so verification against a static
  * committee (config/src/lib.rs:140-143) needs no decompression of A and no
  * doublings.  Keys are addressed by index (the caller's committee order);
@@ -124,7 +129,7 @@ int nt_keyset_create(nt_ctx *ctx, const uint8_t *pk32, uint32_t nkeys, nt_keyset
 void nt_keyset_free(nt_keyset *ks);
 /* flags of key i: bit 0 = decodes, bit 1 = small order */
 int nt_keyset_flags(const nt_keyset *ks, uint32_t i, uint32_t *flags);
-/* comb digit width of the set (16 or 20) and its device bytes per device */
+/* comb digit width of the set (16, 18 or 20) and its device bytes per device */
 int nt_keyset_info(const nt_keyset *ks, uint32_t *comb_bits, uint64_t *bytes_per_device);
 int nt_ed25519_verify_keyset(nt_ctx *ctx, const nt_keyset *ks, int mode, const uint32_t *key_idx,
                              const uint8_t *sig64, const uint8_t *msg, const uint64_t *off,

@@ -377,6 +377,7 @@ hipError_t launch_wcomb_build(int bits, const uint32_t* d_enc, uint32_t nkeys, i
   if (batch == 0) return hipErrorInvalidValue;
   switch (bits) {
     case kKeyCombWide: return wcomb_build<kKeyCombWide>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
+    case kKeyCombMid: return wcomb_build<kKeyCombMid>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
     case kKeyCombNarrow:
       return wcomb_build<kKeyCombNarrow>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
     default: return hipErrorInvalidValue;
@@ -402,6 +403,10 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
       e = mode == kStrict   ? launch_keyset_m<kStrict, kKeyCombWide>(NT_KS_ARGS)
           : mode == kMixed  ? launch_keyset_m<kMixed, kKeyCombWide>(NT_KS_ARGS)
                             : launch_keyset_m<kCofactorless, kKeyCombWide>(NT_KS_ARGS);
+    else if (key_bits == kKeyCombMid)
+      e = mode == kStrict   ? launch_keyset_m<kStrict, kKeyCombMid>(NT_KS_ARGS)
+          : mode == kMixed  ? launch_keyset_m<kMixed, kKeyCombMid>(NT_KS_ARGS)
+                            : launch_keyset_m<kCofactorless, kKeyCombMid>(NT_KS_ARGS);
     else if (key_bits == kKeyCombNarrow)
       e = mode == kStrict   ? launch_keyset_m<kStrict, kKeyCombNarrow>(NT_KS_ARGS)
           : mode == kMixed  ? launch_keyset_m<kMixed, kKeyCombNarrow>(NT_KS_ARGS)
@@ -425,8 +430,10 @@ static size_t comb_size(int what) {
   }
 }
 static size_t comb_size(int bits, int what) {
-  return bits == kKeyCombWide ? comb_size<kKeyCombWide>(what)
-         : bits == kKeyCombNarrow ? comb_size<kKeyCombNarrow>(what) : 0;
+  return bits == kKeyCombWide     ? comb_size<kKeyCombWide>(what)
+         : bits == kKeyCombMid    ? comb_size<kKeyCombMid>(what)
+         : bits == kKeyCombNarrow ? comb_size<kKeyCombNarrow>(what)
+                                  : 0;
 }
 size_t wcomb_bytes_per_key(int bits) { return comb_size(bits, 0); }
 size_t wcomb_bases_bytes_per_key(int bits) { return comb_size(bits, 1); }

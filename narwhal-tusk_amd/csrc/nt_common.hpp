@@ -32,6 +32,7 @@ enum VerifyMode : int {
 
 // Digit widths of the committee-key combs (ed25519_ops.hpp, wide combs)
 constexpr int kKeyCombWide = 20;    // 13 additions per [k]A, 872 MB per key: used when they fit in HBM
+constexpr int kKeyCombMid = 18;     // 15 additions, 252 MB per key (NT_KEYSET_COMB_BITS=18, A/B)
 constexpr int kKeyCombNarrow = 16;  // 16 additions, 67 MB per key
 
 }  // namespace nt

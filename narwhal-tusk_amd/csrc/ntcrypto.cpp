@@ -295,7 +295,7 @@ struct nt_keyset {
   nt_ctx* ctx = nullptr;
   uint32_t nkeys = 0;
   std::vector<uint8_t> enc;     // host copy of the key encodings (small-call path)
-  int bits = 0;                 // comb digit width of every key (nt::kKeyCombWide / kKeyCombNarrow)
+  int bits = 0;                 // comb digit width of every key (nt::kKeyComb{Wide,Mid,Narrow})
   std::vector<uint32_t> flags;  // host copy of kKey* bits
   struct PerDev {
     int ordinal = -1;
@@ -1124,11 +1124,12 @@ int nt_ed25519_keypair_batch(nt_ctx* ctx, const uint8_t* seed32, uint64_t n, uin
 // ---- committee key cache --------------------------------------------------
 // Comb width of a new key set: 20-bit combs (13 additions per [k]A, 872 MB per
 // key) when every device can hold them and keep 1/8 of its HBM free, else
-// 16-bit combs (16 additions, 67 MB per key).  NT_KEYSET_COMB_BITS=16|20 forces one.
+// 16-bit combs (16 additions, 67 MB per key).  NT_KEYSET_COMB_BITS=16|18|20 forces
+// one (18 bits: 15 additions, 252 MB per key).
 static int keyset_comb_bits(nt_ctx* ctx, uint32_t nkeys) {
   if (const char* e = std::getenv("NT_KEYSET_COMB_BITS")) {
     const int b = std::atoi(e);
-    if (b == nt::kKeyCombWide || b == nt::kKeyCombNarrow) return b;
+    if (b == nt::kKeyCombWide || b == nt::kKeyCombMid || b == nt::kKeyCombNarrow) return b;
   }
   const size_t need = nt::wcomb_bytes_per_key(nt::kKeyCombWide) * std::max<uint32_t>(nkeys, 1) +
                       nt::wcomb_fill_tmp_bytes_per_key(nt::kKeyCombWide) * nt::wcomb_fill_batch(nt::kKeyCombWide);
