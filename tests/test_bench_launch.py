@@ -4,10 +4,12 @@ torch.distributed.run, one process per GPU, LOCAL_RANK = device ordinal.
 CPU only: the argv/env of the launcher, and a real 2-rank launch in the
 rank-probe mode (each rank reports its layout and exits before any GPU call)."""
 import json
-import re
 import os
+import re
 import subprocess
 import sys
+
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -38,3 +40,23 @@ def test_two_rank_launch_probe():
     assert sorted(x["rank"] for x in lines) == [0, 1]
     assert all(x["world"] == 2 for x in lines)
     assert sorted(x["device"] for x in lines) == [0, 1]  # LOCAL_RANK -> device ordinal
+
+
+@pytest.mark.gpu
+def test_two_rank_bench_on_one_gpu():
+    """The driver's N>1 path end to end on the GPU box (both ranks pinned to
+    device 0 by NT_BENCH_DEVICE): one JSON line with n_gpus 2, both ranks'
+    verdicts checked, no mismatches."""
+    env = dict(os.environ, NT_BENCH_DEVICE="0")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--sigs", "8192", "--certs", "2000", "--committee", "10", "--sha-msgs", "256",
+                        "--sha-len", "20000", "--no-cpu", "--no-latency", "--no-ingest"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in re.findall(r"^\{.*\}$", r.stdout, re.M)]
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["parity"] == {"mismatches_vs_expected": 0, "checked": 2 * 8192}
+    assert d["certificates"]["keyset"]["mismatches_vs_expected"] == 0
+    assert d["sha512"]["spot_check_ok"]
