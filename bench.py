@@ -608,6 +608,17 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
     mbits = torch.zeros(((V + G + 63) // 64 + 1,), dtype=torch.int64, device=dev)
 
     fused = os.environ.get("NT_BENCH_FUSED", "1") != "0"
+    # layout experiment (A/B only): the fused launch sees the votes grouped by
+    # committee key, so a wave's comb lookups stay within one key's table
+    keysort = fused and os.environ.get("NT_BENCH_KEYSORT") == "1"
+    perm = None
+    if keysort:
+        perm = torch.argsort(vkey, stable=True)
+        mkey[:V] = vkey[perm]
+        msig[:V] = vsig[perm]
+        m_off[:V] = v_off[perm]
+        m_len[:V] = v_len[perm]
+        perm = perm.cpu().numpy()
 
     def step(cached):
         be.dev_sha512(0, sp, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, hd2.data_ptr())
@@ -631,6 +642,11 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
 
     def verdicts(cached):
         gb = np.unpackbits(gbits.cpu().numpy().view(np.uint8), bitorder="little")[:G].astype(bool)
+        if cached and keysort:   # un-permute the vote bits, AND per certificate on the host
+            vb = np.unpackbits(mbits.cpu().numpy().view(np.uint8), bitorder="little")[:V].astype(bool)
+            orig = np.empty(V, bool)
+            orig[perm] = vb
+            gb = orig.reshape(G, quorum).all(axis=1)
         if cached and fused:   # header verdicts follow the V vote bits of the fused launch
             hb = np.unpackbits(mbits.cpu().numpy().view(np.uint8), bitorder="little")[V:V + G].astype(bool)
         else:

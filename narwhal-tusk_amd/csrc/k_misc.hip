@@ -378,6 +378,7 @@ hipError_t launch_wcomb_build(int bits, const uint32_t* d_enc, uint32_t nkeys, i
   switch (bits) {
     case kKeyCombWide: return wcomb_build<kKeyCombWide>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
     case kKeyCombMid: return wcomb_build<kKeyCombMid>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
+    case 24: return wcomb_build<24>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);  // B only
     case kKeyCombNarrow:
       return wcomb_build<kKeyCombNarrow>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
     default: return hipErrorInvalidValue;
@@ -387,17 +388,142 @@ hipError_t launch_wcomb_build(int bits, const uint32_t* d_enc, uint32_t nkeys, i
 // signatures per key-cache launch (a multiple of 64: verdict words stay aligned)
 constexpr uint64_t kKsMaxPerLaunch = 8ull << 20;
 
+// --------------------------------------------------------------------------
+// Key-grouped order for key-cache launches.  A wave's 256 signatures verified
+// against 64+ different committee keys make every comb lookup a random 128-B
+// line in a random 2 MB page of an 87 GB table set (translation misses on
+// most of them); grouped by key, a wave walks one key's 872 MB comb.  Measured
+// on config 3 (profiles/r02/ab_keysort): 12.02 -> 9.79 ms per 6.8M-signature
+// launch.  A counting sort by committee index (block-local LDS ranks, one
+// global reservation per bucket per block) gives slot -> signature; the
+// kernel writes one verdict byte at the signature's own index and
+// k_pack_bytes turns them into the caller's 64-bit ballot words.
+// --------------------------------------------------------------------------
+constexpr uint32_t kSortBuckets = 4096;  // committee keys + 1 "unknown" bucket
+constexpr uint64_t kSortMin = 65536;     // smaller launches keep the input order
+constexpr int kSortTile = 16;            // items per thread of k_key_scatter
+
+NT_D NT_INLINE uint32_t sort_bucket(uint32_t k, int mixed, uint32_t nkeys) {
+  if (mixed) k &= ~kKeyWantStrict;
+  return k < nkeys ? k : nkeys;
+}
+
+__global__ __launch_bounds__(kBlock) void k_key_hist(const uint32_t* __restrict__ key, uint64_t n, int mixed,
+                                                    uint32_t nkeys, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[kSortBuckets];
+  for (uint32_t b = threadIdx.x; b <= nkeys; b += kBlock) h[b] = 0;
+  __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
+    atomicAdd(&h[sort_bucket(key[i], mixed, nkeys)], 1u);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b <= nkeys; b += kBlock)
+    if (h[b]) atomicAdd(&hist[b], h[b]);
+}
+
+// exclusive scan of nb <= kSortBuckets counts (one workgroup; ~4k adds)
+__global__ __launch_bounds__(kBlock) void k_key_scan(const uint32_t* __restrict__ hist, uint32_t nb,
+                                                    uint32_t* __restrict__ cursor) {
+  __shared__ uint32_t part[kBlock];
+  const uint32_t per = (nb + kBlock - 1) / kBlock, b0 = threadIdx.x * per;
+  uint32_t sum = 0;
+  for (uint32_t b = b0; b < b0 + per && b < nb; ++b) sum += hist[b];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int t = 0; t < kBlock; ++t) {
+      const uint32_t v = part[t];
+      part[t] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+  uint32_t acc = part[threadIdx.x];
+  for (uint32_t b = b0; b < b0 + per && b < nb; ++b) {
+    cursor[b] = acc;
+    acc += hist[b];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_key_scatter(const uint32_t* __restrict__ key, uint64_t n, int mixed,
+                                                       uint32_t nkeys, uint32_t* __restrict__ cursor,
+                                                       uint32_t* __restrict__ perm) {
+  __shared__ uint32_t cnt[kSortBuckets];
+  __shared__ uint32_t base[kSortBuckets];
+  for (uint32_t b = threadIdx.x; b <= nkeys; b += kBlock) cnt[b] = 0;
+  __syncthreads();
+  const uint64_t t0 = (uint64_t)blockIdx.x * kBlock * kSortTile;
+  uint32_t bk[kSortTile], rk[kSortTile];
+#pragma unroll
+  for (int r = 0; r < kSortTile; ++r) {
+    const uint64_t i = t0 + (uint64_t)r * kBlock + threadIdx.x;
+    bk[r] = i < n ? sort_bucket(key[i], mixed, nkeys) : 0u;
+    rk[r] = i < n ? atomicAdd(&cnt[bk[r]], 1u) : 0u;
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b <= nkeys; b += kBlock)
+    if (cnt[b]) base[b] = atomicAdd(&cursor[b], cnt[b]);
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kSortTile; ++r) {
+    const uint64_t i = t0 + (uint64_t)r * kBlock + threadIdx.x;
+    if (i < n) perm[base[bk[r]] + rk[r]] = (uint32_t)i;
+  }
+}
+
+// verdict bytes -> 64-bit ballot words
+__global__ __launch_bounds__(kBlock) void k_pack_bytes(const uint8_t* __restrict__ b, uint64_t n,
+                                                      unsigned long long* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const unsigned long long bal = __ballot(i < n && b[i] != 0);
+  const uint64_t wbase = i & ~(uint64_t)63;
+  if ((threadIdx.x & 63u) == 0 && wbase < n) out[wbase >> 6] = bal;
+}
+
+static bool keyset_sort_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NT_KEYSET_SORT");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
+size_t keyset_sort_bytes(uint64_t n) {
+  const uint64_t m = n < kKsMaxPerLaunch ? n : kKsMaxPerLaunch;
+  return 2 * kSortBuckets * 4 + (size_t)m * 5 + 64;
+}
+
 hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                                 const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                                 const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
-                                const uint32_t* d_combB, void* d_stash, uint64_t* d_out_words, hipStream_t s) {
+                                const uint32_t* d_combB, void* d_stash, void* d_sort, uint64_t* d_out_words,
+                                hipStream_t s) {
   // launches of at most kKsMaxPerLaunch signatures reuse one stash (stream-ordered)
   for (uint64_t lo = 0; lo < n; lo += kKsMaxPerLaunch) {
     const uint64_t m = n - lo < kKsMaxPerLaunch ? n - lo : kKsMaxPerLaunch;
     const uint64_t blocks = keyset_blocks(m);
+    const uint32_t* perm = nullptr;
+    uint8_t* bytes = nullptr;
+    if (d_sort && keyset_sort_enabled() && m >= kSortMin && nkeys + 1 <= kSortBuckets) {
+      uint32_t* hist = (uint32_t*)d_sort;
+      uint32_t* cursor = hist + kSortBuckets;
+      uint32_t* p = cursor + kSortBuckets;
+      bytes = (uint8_t*)(p + m);
+      const int mixed = mode == kMixed;
+      hipError_t e = hipMemsetAsync(hist, 0, 4ull * (nkeys + 1), s);
+      if (e != hipSuccess) return e;
+      const uint32_t hb = (uint32_t)((m + kBlock - 1) / kBlock < 2048 ? (m + kBlock - 1) / kBlock : 2048);
+      hipLaunchKernelGGL(k_key_hist, dim3(hb), dim3(kBlock), 0, s, d_key_idx + lo, m, mixed, nkeys, hist);
+      hipLaunchKernelGGL(k_key_scan, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)hist, nkeys + 1, cursor);
+      const uint64_t sb = (m + (uint64_t)kBlock * kSortTile - 1) / ((uint64_t)kBlock * kSortTile);
+      hipLaunchKernelGGL(k_key_scatter, dim3((uint32_t)sb), dim3(kBlock), 0, s, d_key_idx + lo, m, mixed, nkeys, cursor,
+                         p);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      perm = p;
+    }
 #define NT_KS_ARGS                                                                                           \
   blocks, d_key_idx + lo, d_sig + 64 * lo, d_msg, d_off + lo, d_len + lo, m, d_meta, d_enc, d_combA, nkeys, \
-      d_combB, d_stash, d_out_words + lo / 64, s
+      d_combB, d_stash, d_out_words + lo / 64, perm, bytes, s
     hipError_t e;
     if (key_bits == kKeyCombWide)
       e = mode == kStrict   ? launch_keyset_m<kStrict, kKeyCombWide>(NT_KS_ARGS)
@@ -415,6 +541,11 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
       e = hipErrorInvalidValue;
 #undef NT_KS_ARGS
     if (e != hipSuccess) return e;
+    if (perm) {
+      hipLaunchKernelGGL(k_pack_bytes, dim3((uint32_t)((m + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                         (const uint8_t*)bytes, m, (unsigned long long*)(d_out_words + lo / 64));
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
   }
   return hipSuccess;
 }
@@ -433,6 +564,7 @@ static size_t comb_size(int bits, int what) {
   return bits == kKeyCombWide     ? comb_size<kKeyCombWide>(what)
          : bits == kKeyCombMid    ? comb_size<kKeyCombMid>(what)
          : bits == kKeyCombNarrow ? comb_size<kKeyCombNarrow>(what)
+         : bits == 24             ? comb_size<24>(what)
                                   : 0;
 }
 size_t wcomb_bytes_per_key(int bits) { return comb_size(bits, 0); }

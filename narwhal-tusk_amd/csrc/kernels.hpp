@@ -29,7 +29,10 @@ hipError_t launch_wcomb_build(int bits, const uint32_t* d_enc, uint32_t nkeys, i
 hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                                 const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                                 const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
-                                const uint32_t* d_combB, void* d_stash, uint64_t* d_out_words, hipStream_t s);
+                                const uint32_t* d_combB, void* d_stash, void* d_sort, uint64_t* d_out_words,
+                                hipStream_t s);
+// scratch of launch_verify_keyset's key-grouped order (d_sort; may be null = input order)
+size_t keyset_sort_bytes(uint64_t n);
 // key-cache verification: blocks of a launch over n signatures and the per-lane
 // stash it needs (d_stash above)
 uint64_t keyset_round_sigs(uint32_t cus);

@@ -150,7 +150,8 @@ template <int MODE, int WA>
 hipError_t launch_keyset_m(uint64_t blocks, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                            const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                            const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
-                           const uint32_t* d_combB, void* d_stash, uint64_t* d_out_words, hipStream_t s);
+                           const uint32_t* d_combB, void* d_stash, uint64_t* d_out_words, const uint32_t* d_perm,
+                           uint8_t* d_out_bytes, hipStream_t s);
 int keyset_occupancy();
 
 // Occupancy variants (waves per SIMD the register allocator targets), chosen

@@ -87,7 +87,7 @@ bool is_pinned(const void* p, uint64_t bytes) {
   return (uintptr_t)p + bytes <= it->first + it->second;
 }
 
-enum { B_DATA, B_OFF, B_LEN, B_PK, B_SIG, B_OUT, B_OUT2, B_FIRST, B_CNT, B_STASH, B_NBUF };
+enum { B_DATA, B_OFF, B_LEN, B_PK, B_SIG, B_OUT, B_OUT2, B_FIRST, B_CNT, B_STASH, B_SORT, B_NBUF };
 
 struct Device {
   int ordinal = -1;
@@ -110,7 +110,7 @@ struct Device {
   // verify workspace and key-cache stash.
   hipStream_t stream2 = nullptr;
   hipEvent_t join2 = nullptr, ws2_done = nullptr;
-  DevBuf ws2, stash2;
+  DevBuf ws2, stash2, sort2;
   std::mutex mu;
   DevBuf d[B_NBUF];
   HostBuf h[B_NBUF];
@@ -141,6 +141,7 @@ struct Device {
     if (stream2 && stream2 != stream) (void)hipStreamSynchronize(stream2);
     if (ws2.p) (void)hipFree(ws2.p);
     if (stash2.p) (void)hipFree(stash2.p);
+    if (sort2.p) (void)hipFree(sort2.p);
     if (join2) (void)hipEventDestroy(join2);
     if (ws2_done) (void)hipEventDestroy(ws2_done);
     if (stream2 && stream2 != stream) (void)hipStreamDestroy(stream2);
@@ -260,6 +261,7 @@ struct Device {
   // Key-cache launch on stream s with stash st: launches that use the shared
   // d[B_STASH] (host chunks on `stream`, device-API calls on any stream) wait
   // for its previous user and mark it, like d_ws; stash2 belongs to stream2.
+  // The key-grouping scratch (d[B_SORT] / sort2) goes with its stash.
   template <class F>
   int keyset_launch(hipStream_t s, void* st, F&& launch) {
     const bool shared = st == d[B_STASH].p;
@@ -988,7 +990,9 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
       uint64_t mc = 0;
       for (size_t c = 0; c < C; ++c) mc = std::max(mc, E[c + 1] - E[c]);
       NT_CHK(dv.d[B_STASH].ensure(nt::keyset_stash_bytes(mc)));
+      NT_CHK(dv.d[B_SORT].ensure(nt::keyset_sort_bytes(mc)));
       if (C > 1) NT_CHK(dv.stash2.ensure(nt::keyset_stash_bytes(mc)));
+      if (C > 1) NT_CHK(dv.sort2.ensure(nt::keyset_sort_bytes(mc)));
       pd_meta = &ks->dev[dev_index(ctx, dv)];
     }
     uint8_t* hkey = dv.h[B_PK].as<uint8_t>();
@@ -1026,9 +1030,10 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
         if (ks) {
           const auto& pd = *(const nt_keyset::PerDev*)pd_meta;
           void* st = (c & 1) ? dv.stash2.p : dv.d[B_STASH].p;
+          void* so = (c & 1) ? dv.sort2.p : dv.d[B_SORT].p;
           NT_CHK(dv.keyset_launch(s, st, [&] {
             return nt::launch_verify_keyset(NT_MODE_COFACTORLESS, ks->bits, (const uint32_t*)dk, dsig, dmsg, doff, dlen,
-                                            mc, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, st, dout, s);
+                                            mc, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, st, so, dout, s);
           }));
         } else {
           NT_CHK(dv.verify_chunk((int)c, NT_MODE_COFACTORLESS, dk, dsig, dmsg, doff, dlen, mc, dout));
@@ -1238,7 +1243,9 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
     uint64_t mc = 0;
     for (const auto& c : ch) mc = std::max(mc, c.second - c.first);
     NT_CHK(dv.d[B_STASH].ensure(nt::keyset_stash_bytes(mc)));
+    NT_CHK(dv.d[B_SORT].ensure(nt::keyset_sort_bytes(mc)));
     if (ch.size() > 1) NT_CHK(dv.stash2.ensure(nt::keyset_stash_bytes(mc)));
+    if (ch.size() > 1) NT_CHK(dv.sort2.ensure(nt::keyset_sort_bytes(mc)));
     for (size_t c = 0; c < ch.size(); ++c) {
       const uint64_t a = ch[c].first, b = ch[c].second;
       NT_CHK(msg_copy(dv, msg, off, len, lo, ms, c, a, b));
@@ -1248,12 +1255,13 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
                             hipMemcpyHostToDevice, dv.cstream));
       NT_TRY(dv.fence((int)c));
       void* st = (c & 1) ? dv.stash2.p : dv.d[B_STASH].p;
+      void* so = (c & 1) ? dv.sort2.p : dv.d[B_SORT].p;
       hipStream_t s = dv.cstr((int)c);
       NT_CHK(dv.keyset_launch(s, st, [&] {
         return nt::launch_verify_keyset(mode, ks->bits, dv.d[B_PK].as<uint32_t>() + a,
                                         dv.d[B_SIG].as<uint8_t>() + 64 * a, dv.d[B_DATA].as<uint8_t>(),
                                         dv.d[B_OFF].as<uint64_t>() + a, dv.d[B_LEN].as<uint64_t>() + a, b - a,
-                                        pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, st,
+                                        pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, st, so,
                                         dv.d[B_OUT].as<uint64_t>() + a / 64, s);
       }));
     }
@@ -1334,10 +1342,12 @@ int nt_dev_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int dev, void
   // every other user by stash_done, whatever the streams
   std::lock_guard<std::mutex> lk(dv->mu);
   NT_CHK(dv->d[B_STASH].ensure(nt::keyset_stash_bytes(n)));
+  NT_CHK(dv->d[B_SORT].ensure(nt::keyset_sort_bytes(n)));
   void* stash = dv->d[B_STASH].p;
+  void* so = dv->d[B_SORT].p;
   return dv->keyset_launch(s, stash, [&] {
     return nt::launch_verify_keyset(mode, ks->bits, d_key_idx, d_sig64, d_msg, d_off, d_len, n, pd.d_meta, pd.d_enc,
-                                    pd.d_comb, ks->nkeys, dv->d_combB, stash, d_out_words, s);
+                                    pd.d_comb, ks->nkeys, dv->d_combB, stash, so, d_out_words, s);
   });
 }
 

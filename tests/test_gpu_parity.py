@@ -291,3 +291,44 @@ def test_keyset_committee_random_vs_oracle(be, oracle):
     flags = [ks.flags(i) for i in range(nk)]
     assert all(f == 1 for f in flags)
     ks.close()
+
+
+@pytest.mark.gpu
+def test_keyset_key_grouped_order(be, corpus, monkeypatch):
+    """Key-cache launches of >= 65,536 signatures verify in key-grouped order
+    (k_misc.hip: counting sort by committee index, verdict bytes scattered back
+    to each signature's own index, packed into ballot words).  The corpus tiled
+    to 72k signatures -- every edge case, unknown key indices, per-signature
+    strictness -- must give the same verdict per signature as the corpus labels,
+    and tiled certificate groups the fixture's group verdicts."""
+    import ntcrypto
+    monkeypatch.setenv("NT_KEYSET_COMB_BITS", "16")
+    uniq, inv = np.unique(corpus["pk"], axis=0, return_inverse=True)
+    inv = inv.ravel().astype(np.uint32)
+    ks = be.keyset(uniq)
+    reps = 200
+    n0 = len(inv)
+    idx = np.tile(inv, reps)
+    unknown = (np.arange(n0 * reps) % 97) == 5
+    idx[unknown] = len(uniq) + 3                      # not a committee key -> reject
+    want_strict = (np.arange(n0 * reps) % 3) == 1
+    midx = (idx | np.where(want_strict, np.uint32(ntcrypto.NT_KEY_STRICT_BIT), np.uint32(0))).astype(np.uint32)
+    sig = np.tile(corpus["sig"], (reps, 1))
+    off = np.tile(corpus["off"], reps)
+    ln = np.tile(corpus["len"], reps)
+    got = ks.verify(ntcrypto.NT_MODE_MIXED, midx, sig, corpus["msg"], off, ln)
+    want = np.where(np.tile(want_strict.reshape(reps, n0)[0], reps), np.tile(corpus["strict"], reps),
+                    np.tile(corpus["batch_rule"], reps)).astype(bool) & ~unknown
+    assert np.array_equal(got, want)
+    ks.close()
+    g = np.load(os.path.join(GOLD, "batch_groups.npz"))
+    u2, inv2 = np.unique(g["pk"], axis=0, return_inverse=True)
+    ks = be.keyset(u2)
+    nsig = len(g["pk"])
+    reps = -(-70000 // nsig)
+    first = np.concatenate([g["first"] + r * nsig for r in range(reps)]).astype(np.uint64)
+    cnt = np.tile(g["cnt"], reps)
+    kidx = np.tile(inv2.astype(np.uint32).ravel(), reps)
+    gb = ks.verify_batch_groups(kidx, np.tile(g["sig"], (reps, 1)), first, cnt, np.tile(g["msg32"], (reps, 1)))
+    assert np.array_equal(gb, np.tile(g["expect"], reps).astype(bool))
+    ks.close()
