@@ -46,7 +46,7 @@ sys.path.insert(0, os.path.join(ROOT, "narwhal-tusk_amd"))
 METRIC = "Ed25519 verifies/sec + SHA-512 GB/s at 1/2/4/8 MI355X vs dalek host-core base"
 MAD_PEAK_TS = 256 * 4 * 64 * 2.4e9 / 4 / 1e12  # v_mad_u64_u32: 4 cycles per wave64 per SIMD
 HBM_PEAK_GBS = 8000.0
-PMC_PROFILE = os.path.join("r01", "pmc_v9.json")  # tools/profile_round.sh + tools/pmc_summarize.py
+PMC_PROFILE = os.path.join("r02", "pmc_verify_sha.json")  # tools/profile_round.sh + tools/pmc_summarize.py
 PMC_N = 1_000_000  # signatures per launch in that profile (the default config-2 run)
 SODIUM = "/opt/conda/lib/libsodium.so.23"
 

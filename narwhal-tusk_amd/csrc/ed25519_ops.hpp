@@ -467,13 +467,15 @@ NT_HD NT_INLINE uint32_t compare_one(const ge_p2& P, const fe& zi, const uint32_
 //   st.put(j, P, prefix) / st.get_point(j, P) /  per-lane stash of R'_j and the
 //   st.get_prefix(j, prefix)                     running product Z_0 .. Z_j
 // Returns bit j = verdict of signature j.  The stash keeps the registers of a
-// lane independent of N (the kernel's stash lives in global memory).
+// lane independent of N (the kernel's stash lives in global memory); m <= N
+// signatures are run (the kernel's run-time per-lane count).
 template <int MODE, int N, class Loader, class WCombB, class Stash>
-NT_HD NT_INLINE uint32_t verify_cached_batch(const Loader& ld, const WCombB& cb, Stash& st) {
+NT_HD NT_INLINE uint32_t verify_cached_batch(const Loader& ld, const WCombB& cb, Stash& st, int m = N) {
+  static_assert(N >= 1 && N <= 32, "verdict bits of a lane are one word");
   uint32_t okbits = 0, strictbits = 0;
   fe acc;
 #pragma unroll 1
-  for (int j = 0; j < N; ++j) {
+  for (int j = 0; j < m; ++j) {
     uint32_t meta, Aw[8], Rw[8], Sw[8];
     const uint8_t* msg;
     uint64_t len;
@@ -491,7 +493,7 @@ NT_HD NT_INLINE uint32_t verify_cached_batch(const Loader& ld, const WCombB& cb,
   fe inv;
   fe_invert(inv, acc);
 #pragma unroll 1
-  for (int j = N - 1; j >= 0; --j) {
+  for (int j = m - 1; j >= 0; --j) {
     ge_p2 P;
     fe zi;
     st.get_point(j, P);

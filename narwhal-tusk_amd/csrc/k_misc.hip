@@ -10,7 +10,7 @@
 //                         (per-entry rule of crypto/src/lib.rs:206-219 -> dalek verify_batch,
 //                         SURVEY.md A.3); one verdict bit per signature (64-bit ballot words)
 //   k_ed25519_verify_keyset<M>  the same against a committee key cache (wide combs of -A),
-//                         four signatures per lane sharing one inversion
+//                         up to eight signatures per lane sharing one inversion
 //   k_group_and           AND of per-signature bits over each certificate's vote range
 //   k_group_msgs          per-signature message offset/length of certificate groups
 //   k_ed25519_sign        keygen + RFC 8032 signing (corpus generation / SignatureService
@@ -501,7 +501,8 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
   // launches of at most kKsMaxPerLaunch signatures reuse one stash (stream-ordered)
   for (uint64_t lo = 0; lo < n; lo += kKsMaxPerLaunch) {
     const uint64_t m = n - lo < kKsMaxPerLaunch ? n - lo : kKsMaxPerLaunch;
-    const uint64_t blocks = keyset_blocks(m);
+    const uint32_t per_lane = keyset_per_lane();
+    const uint64_t blocks = keyset_blocks(m, per_lane);
     const uint32_t* perm = nullptr;
     uint8_t* bytes = nullptr;
     if (d_sort && keyset_sort_enabled() && m >= kSortMin && nkeys + 1 <= kSortBuckets) {
@@ -523,7 +524,7 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
     }
 #define NT_KS_ARGS                                                                                           \
   blocks, d_key_idx + lo, d_sig + 64 * lo, d_msg, d_off + lo, d_len + lo, m, d_meta, d_enc, d_combA, nkeys, \
-      d_combB, d_stash, d_out_words + lo / 64, perm, bytes, s
+      d_combB, d_stash, d_out_words + lo / 64, perm, bytes, per_lane, s
     hipError_t e;
     if (key_bits == kKeyCombWide)
       e = mode == kStrict   ? launch_keyset_m<kStrict, kKeyCombWide>(NT_KS_ARGS)
@@ -581,12 +582,23 @@ uint64_t verify_grid(uint64_t n, uint32_t ws_slots) {
 
 // signatures one wave of resident workgroups covers (every CU full at the
 // kernel's occupancy): launches sized in whole rounds leave no partial last wave
-uint64_t keyset_round_sigs(uint32_t cus) { return (uint64_t)cus * 4 * keyset_occ() * 64 * kKsPerLane; }
+uint64_t keyset_round_sigs(uint32_t cus) { return (uint64_t)cus * 4 * keyset_occ() * 64 * keyset_per_lane(); }
 uint64_t verify_round_sigs(uint32_t cus) { return (uint64_t)cus * verify_occupancy() * 2 * kBlock; }
-uint64_t keyset_blocks(uint64_t n) { return (n + kKsPerLane * kBlock - 1) / (kKsPerLane * kBlock); }
-// stash of one launch (<= kKsMaxPerLaunch signatures: 1.25 GiB at most)
+// signatures per lane of a key-cache launch (one inversion each): 8 (the
+// 4 / 6 / 8 / 12 / 16 A/B in DESIGN.md §5.2); NT_KEYSET_PER_LANE in
+// [1, kKsPerLane] overrides it for A/B runs
+uint32_t keyset_per_lane() {
+  static const uint32_t m = (uint32_t)env_occ("NT_KEYSET_PER_LANE", kKsPerLane, 1, kKsPerLane);
+  return m;
+}
+uint64_t keyset_blocks(uint64_t n, uint32_t per_lane) {
+  return (n + (uint64_t)per_lane * kBlock - 1) / ((uint64_t)per_lane * kBlock);
+}
+// stash of one launch (<= kKsMaxPerLaunch signatures: 1.25 GiB at most):
+// blocks * per_lane * kBlock <= n + per_lane * kBlock slots of kKsQuads quads
 size_t keyset_stash_bytes(uint64_t n) {
-  return (size_t)keyset_blocks(n < kKsMaxPerLaunch ? n : kKsMaxPerLaunch) * kKsStashQuadsPerBlock * 16;
+  const uint64_t m = n < kKsMaxPerLaunch ? n : kKsMaxPerLaunch;
+  return (size_t)(m + (uint64_t)kKsPerLane * kBlock) * kKsQuads * 16;
 }
 size_t ws_bytes_per_slot() { return (size_t)kAEntries * kAQuads * kBlock * 16; }
 

@@ -38,7 +38,8 @@ size_t keyset_sort_bytes(uint64_t n);
 uint64_t keyset_round_sigs(uint32_t cus);
 uint64_t verify_grid(uint64_t n, uint32_t ws_slots);  // blocks of a launch_verify
 uint64_t verify_round_sigs(uint32_t cus);
-uint64_t keyset_blocks(uint64_t n);
+uint32_t keyset_per_lane();
+uint64_t keyset_blocks(uint64_t n, uint32_t per_lane);
 size_t keyset_stash_bytes(uint64_t n);
 size_t wcomb_bytes_per_key(int bits);
 size_t wcomb_bases_bytes_per_key(int bits);

@@ -96,16 +96,18 @@ struct WsATab {
   }
 };
 
-// ---- key-cache verification: 4 signatures per lane, one inversion ----------
+// ---- key-cache verification: up to 8 signatures per lane, one inversion -----
 #ifndef NT_KS_PER_LANE
-#define NT_KS_PER_LANE 4
+#define NT_KS_PER_LANE 8
 #endif
-constexpr int kKsPerLane = NT_KS_PER_LANE;  // signatures per lane sharing one inversion
+// most signatures per lane sharing one inversion; a launch runs
+// keyset_per_lane() <= kKsPerLane of them (a kernel argument)
+constexpr int kKsPerLane = NT_KS_PER_LANE;
 constexpr int kKsQuads = 10;  // X, Y, Z, prefix: 40 words per (signature, lane)
-constexpr size_t kKsStashQuadsPerBlock = (size_t)kKsPerLane * kKsQuads * kBlock;
 
 // Per-lane stash in global memory, layout [block][j][quad][lane] of uint4
-// (lane-minor: a wave's 16-byte accesses are contiguous).
+// (lane-minor: a wave's 16-byte accesses are contiguous); a block's region is
+// per_lane * kKsQuads * kBlock quads.
 struct KsStash {
   uint4* base;  // this block's region
   NT_D NT_INLINE uint4* at(int j, int q) const { return base + ((size_t)(j * kKsQuads + q) * kBlock + threadIdx.x); }
@@ -151,7 +153,7 @@ hipError_t launch_keyset_m(uint64_t blocks, const uint32_t* d_key_idx, const uin
                            const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                            const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
                            const uint32_t* d_combB, void* d_stash, uint64_t* d_out_words, const uint32_t* d_perm,
-                           uint8_t* d_out_bytes, hipStream_t s);
+                           uint8_t* d_out_bytes, uint32_t per_lane, hipStream_t s);
 int keyset_occupancy();
 
 // Occupancy variants (waves per SIMD the register allocator targets), chosen
