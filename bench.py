@@ -45,6 +45,7 @@ sys.path.insert(0, os.path.join(ROOT, "narwhal-tusk_amd"))
 
 METRIC = "Ed25519 verifies/sec + SHA-512 GB/s at 1/2/4/8 MI355X vs dalek host-core base"
 MAD_PEAK_TS = 256 * 4 * 64 * 2.4e9 / 4 / 1e12  # v_mad_u64_u32: 4 cycles per wave64 per SIMD
+MAD_MEASURED_TS = 32.80  # profiles/r01_alu_rate.txt (tools/microbench): 4.80 cycles per wave64 per SIMD
 HBM_PEAK_GBS = 8000.0
 PMC_PROFILE = os.path.join("r02", "pmc_verify_sha.json")  # tools/profile_round.sh + tools/pmc_summarize.py
 PMC_N = 1_000_000  # signatures per launch in that profile (the default config-2 run)
@@ -279,12 +280,18 @@ def main():
     roofline = {"bound": "valu", "achieved": round(achieved, 3), "peak": round(MAD_PEAK_TS, 2),
                 "unit": "Tmad/s (v_mad_u64_u32 32x32->64 multiply-accumulates)",
                 "frac": round(achieved / MAD_PEAK_TS, 4),
+                "measured_mad_rate": MAD_MEASURED_TS,
+                "frac_vs_measured_mad_rate": round(achieved / MAD_MEASURED_TS, 4),
+                "measured_mad_rate_note": "v_mad_u64_u32 throughput of a dependency-free microbenchmark on the "
+                                          "same GPU (profiles/r01_alu_rate.txt: 4.80 cycles per wave-instruction "
+                                          "per SIMD against the nominal 4)",
                 "traffic": pv.get("hbm_bytes_per_launch"),
                 "traffic_note": ("HBM bytes per launch from rocprofv3 FETCH_SIZE*2 + WRITE_SIZE (profiles/%s, "
-                                 "same kernel build, separate --pmc passes; the config-2 launch, grouped by grid size); "
-                                 "algorithmic bytes are ~15.6 KB/verify: 608 B of input, the lane-major per-lane "
-                                 "[j]A/[j]R tables (2,880 B written, ~10.5 KB read) and 13 comb lines of B "
-                                 "(1.7 KB)" % PMC_PROFILE)
+                                 "same kernel build, separate --pmc passes; the config-2 launch, grouped by grid size). "
+                                 "Algorithmic minimum ~2.3 KB/verify (608 B of input + 13 comb lines of B); the rest "
+                                 "(~13.4 KB/verify) is this kernel's own per-lane [j]A/[j]R table workspace (2,880 B "
+                                 "written, ~10.5 KB read), i.e. ~9.6x the minimum -- 2.1 TB/s, not the limiter of an "
+                                 "issue-bound kernel" % PMC_PROFILE)
                 if pv else None,
                 "kernel": "k_ed25519_verify<strict>", "kernel_ms": round(kernel_ms, 3),
                 "mads_per_verify": mads,

@@ -16,7 +16,7 @@
 // when the caller enables it (nt_set_small_call_path), and only below the
 // crossover.  The B table of the host lane is a 12-bit wide comb (22 x 2049
 // affine niels entries = 5.8 MB, built once by wcomb_bases / wcomb_fill on the
-// host) instead of the device's 872 MB 20-bit comb.
+// host) instead of the device's 11.8 GB 24-bit comb.
 #pragma once
 #include <cstddef>
 #include <cstdint>

@@ -45,8 +45,9 @@ NT_HD NT_INLINE void ld8(uint32_t w[8], const uint32_t* p) {
 // Wide combs: for a fixed point P and digit width W, entry (i, j) =
 // j * 2^(W i) * P as affine niels, i in [0, pos), j in [0, 2^(W-1)].  [x]P is
 // then `pos` mixed additions and no doublings (signed radix-2^W digits of x).
-//   W = 20: 13 additions, 872 MB per point  (the base point; committee keys
-//           while they fit: 100 keys = 87 GB of the MI355X's 288 GB of HBM3E)
+//   W = 24: 11 additions, 11.8 GB per point (the base point, one per device)
+//   W = 20: 13 additions, 872 MB per point  (committee keys while they fit:
+//           100 keys = 87 GB of the MI355X's 288 GB of HBM3E)
 //   W = 16: 16 additions,  67 MB per point  (committee keys otherwise)
 // Layout [pos][entry][kWStride words]; a table access type carries its W as
 // `kBits` (WideComb<W> on the device, HostWComb<W> in the host harness).
@@ -54,10 +55,11 @@ NT_HD NT_INLINE void ld8(uint32_t w[8], const uint32_t* p) {
 constexpr int kWStride = 32;  // words per entry (30 used)
 constexpr int kWChunk = 64;   // consecutive entries built by one thread
 #ifndef NT_BCOMB_BITS
-#define NT_BCOMB_BITS 20
+#define NT_BCOMB_BITS 24
 #endif
-constexpr int kBCombBits = NT_BCOMB_BITS;  // comb of the base point B (one per device)
-static_assert(kBCombBits == 16 || kBCombBits == 20 || kBCombBits == 24, "B comb width must be a built width");
+// comb of the base point B (one per device): 24 bits by measurement
+constexpr int kBCombBits = NT_BCOMB_BITS;
+static_assert(kBCombBits == 16 || kBCombBits == 20 || kBCombBits == 22 || kBCombBits == 24, "B comb width must be a built width");
 
 template <int W>
 struct CombGeom {

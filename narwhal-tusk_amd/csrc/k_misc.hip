@@ -19,8 +19,8 @@
 //
 // SIMT design: every lane runs the same window schedule (fixed signed windows,
 // a wave-uniform window count, never per-lane sliding windows), so lanes of a
-// wave never diverge inside the scalar multiplications.  [v s]B is 13 mixed
-// additions from the 872 MB 20-bit wide comb of B (random 128-byte lines, the
+// wave never diverge inside the scalar multiplications.  [v s]B is 11 mixed
+// additions from the 11.8 GB 24-bit wide comb of B (random 128-byte lines, the
 // next one prefetched during the current addition); [u](+-A) + [v](-R) use
 // joint 4-bit windows over per-lane 9-entry cached tables in a global
 // workspace laid out lane-major, so a lookup's loads use whole lines.
@@ -379,6 +379,10 @@ hipError_t launch_wcomb_build(int bits, const uint32_t* d_enc, uint32_t nkeys, i
     case kKeyCombWide: return wcomb_build<kKeyCombWide>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
     case kKeyCombMid: return wcomb_build<kKeyCombMid>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
     case 24: return wcomb_build<24>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);  // B only
+    case 22:  // B only, -DNT_BCOMB_BITS=22 builds (A/B)
+      if constexpr (kBCombBits == 22)
+        return wcomb_build<22>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
+      return hipErrorInvalidValue;
     case kKeyCombNarrow:
       return wcomb_build<kKeyCombNarrow>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
     default: return hipErrorInvalidValue;
@@ -566,6 +570,7 @@ static size_t comb_size(int bits, int what) {
          : bits == kKeyCombMid    ? comb_size<kKeyCombMid>(what)
          : bits == kKeyCombNarrow ? comb_size<kKeyCombNarrow>(what)
          : bits == 24             ? comb_size<24>(what)
+         : bits == 22             ? comb_size<22>(what)
                                   : 0;
 }
 size_t wcomb_bytes_per_key(int bits) { return comb_size(bits, 0); }

@@ -1,8 +1,8 @@
 // ntcrypto.cpp -- host side of the C ABI (include/ntcrypto.h).
 //
 // Owns one `Device` per GPU (per entry of nt_init_devices: a repeated ordinal
-// gets its own): non-blocking HIP streams, the wide comb of B (20-bit digits,
-// 872 MB per Device; 67 MB in a -DNT_BCOMB_BITS=16 build), the per-lane [k]A
+// gets its own): non-blocking HIP streams, the wide comb of B (24-bit digits,
+// 11.8 GB per Device; 872 MB in a -DNT_BCOMB_BITS=20 build), the per-lane [k]A
 // table workspace and grow-only device/pinned staging buffers.
 // Host entry points shard items over devices by contiguous index ranges (one
 // host thread per device), stage through pinned memory, launch, and gather the

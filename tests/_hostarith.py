@@ -29,6 +29,11 @@ def load():
     return _lib
 
 
+def bcomb_bits():
+    """digit width of the comb of B the harness (and the product build) uses"""
+    return int(load().nth_bcomb_bits())
+
+
 def arr(limbs):
     return (ctypes.c_uint32 * 10)(*limbs)
 
@@ -87,21 +92,29 @@ def verify_trivial(mode, pk, sig, msg):
     return bool(load().nth_verify_trivial(mode, pk, sig, msg, ctypes.c_uint64(len(msg))))
 
 
-def verify_cached4(mode, entries, strict_mask=0):
-    """Four (pk, sig, msg) through the key-cache kernel's path: 4 signatures per
-    lane, one inversion (verify_cached_batch<.., 4>).  mode 2 = mixed: entry j
-    is checked strictly iff bit j of strict_mask (the kernel's key_idx bit 31)."""
-    assert len(entries) == 4
+def verify_cached_n(mode, entries, strict_mask=0):
+    """1..8 (pk, sig, msg) through the key-cache kernel's path: n signatures per
+    lane, one inversion (verify_cached_batch, run-time count n).  mode 2 = mixed:
+    entry j is checked strictly iff bit j of strict_mask (the kernel's key_idx
+    bit 31)."""
+    n = len(entries)
+    assert 1 <= n <= 8
     if mode == 2:
         mode = 2 | (strict_mask << 8)
-    out = (ctypes.c_int * 4)()
+    out = (ctypes.c_int * n)()
     msgs = [e[2] for e in entries]
-    mp = (ctypes.c_char_p * 4)(*msgs)
-    lens = (ctypes.c_uint64 * 4)(*[len(m) for m in msgs])
-    rc = load().nth_verify_cached_n(mode, 4, b"".join(e[0] for e in entries), b"".join(e[1] for e in entries),
+    mp = (ctypes.c_char_p * n)(*msgs)
+    lens = (ctypes.c_uint64 * n)(*[len(m) for m in msgs])
+    rc = load().nth_verify_cached_n(mode, n, b"".join(e[0] for e in entries), b"".join(e[1] for e in entries),
                                     mp, lens, out)
     assert rc == 0
     return tuple(bool(x) for x in out)
+
+
+def verify_cached4(mode, entries, strict_mask=0):
+    """Four entries (the round-1 kernel's per-lane count)."""
+    assert len(entries) == 4
+    return verify_cached_n(mode, entries, strict_mask)
 
 
 def sc_halfsize(k: int):

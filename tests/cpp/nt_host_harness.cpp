@@ -231,11 +231,12 @@ void nth_verify_pair(int mode, const uint8_t* pk64, const uint8_t* sig128, const
   out2[0] = (int)ok[0];
   out2[1] = (int)ok[1];
 }
-// The key-cache path (combs of -A_j) for nsig signatures (2 or 4: the kernel
-// runs 4 per lane) through verify_cached_batch with a host stash.
+// The key-cache path (combs of -A_j) for nsig in [1, 8] signatures (the kernel
+// runs keyset_per_lane() = 8 per lane) through verify_cached_batch with a host stash.
+constexpr int kHostKsMax = 8;
 struct HostStash {
-  ge_p2 P[4];
-  fe pre[4];
+  ge_p2 P[kHostKsMax];
+  fe pre[kHostKsMax];
   void put(int j, const ge_p2& p, const fe& a) { P[j] = p; pre[j] = a; }
   void get_point(int j, ge_p2& p) const { p = P[j]; }
   void get_prefix(int j, fe& a) const { a = pre[j]; }
@@ -267,13 +268,13 @@ struct HostLoader {
 };
 int nth_verify_cached_n(int mode, int nsig, const uint8_t* pk, const uint8_t* sig, const uint8_t* const* msgs,
                         const uint64_t* lens, int* out) {
-  if (nsig != 2 && nsig != 4) return -1;
-  alignas(16) uint32_t A[4][8], S[4][16];
+  if (nsig < 1 || nsig > kHostKsMax) return -1;
+  alignas(16) uint32_t A[kHostKsMax][8], S[kHostKsMax][16];
   std::memcpy(A, pk, 32 * nsig);
   std::memcpy(S, sig, 64 * nsig);
-  static HostKeyComb ca[4];
+  static HostKeyComb ca[kHostKsMax];
   const unsigned long long cm = g_fe_mul, cs = g_fe_sq;  // key-cache build is not per signature
-  uint32_t meta[4];
+  uint32_t meta[kHostKsMax];
   for (int j = 0; j < nsig; ++j) {
     meta[j] = key_comb(ca[j], A[j]);
     ca[j].memo.clear();
@@ -286,11 +287,11 @@ int nth_verify_cached_n(int mode, int nsig, const uint8_t* pk, const uint8_t* si
   if ((mode & 0xff) == kMixed) {  // mode = kMixed | strict_mask << 8 (the kernel's key_idx bit 31)
     for (int j = 0; j < nsig; ++j)
       if ((mode >> (8 + j)) & 1) meta[j] |= kKeyWantStrict;
-    bits = nsig == 2 ? verify_cached_batch<kMixed, 2>(ld, bcomb(), st) : verify_cached_batch<kMixed, 4>(ld, bcomb(), st);
-  } else if (nsig == 2) bits = mode == 0 ? verify_cached_batch<kStrict, 2>(ld, bcomb(), st)
-                                  : verify_cached_batch<kCofactorless, 2>(ld, bcomb(), st);
-  else bits = mode == 0 ? verify_cached_batch<kStrict, 4>(ld, bcomb(), st)
-                        : verify_cached_batch<kCofactorless, 4>(ld, bcomb(), st);
+    bits = verify_cached_batch<kMixed, kHostKsMax>(ld, bcomb(), st, nsig);
+  } else {
+    bits = mode == 0 ? verify_cached_batch<kStrict, kHostKsMax>(ld, bcomb(), st, nsig)
+                     : verify_cached_batch<kCofactorless, kHostKsMax>(ld, bcomb(), st, nsig);
+  }
   for (int j = 0; j < nsig; ++j) out[j] = (bits >> j) & 1;
   return 0;
 }
@@ -352,4 +353,5 @@ int nth_small_order(const uint8_t* enc32, int* by_dbl, int* by_y) {
 void nth_counts_reset() { bcomb(); g_fe_mul = g_fe_sq = 0; }
 unsigned long long nth_count_mul() { return g_fe_mul; }
 unsigned long long nth_count_sq() { return g_fe_sq; }
+int nth_bcomb_bits() { return kBCombBits; }
 }

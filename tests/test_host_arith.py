@@ -135,9 +135,10 @@ def test_corpus_through_fallback_ladder():
         assert H.verify_trivial(1, pk, sig, m) == bool(d["batch_rule"][i]), i
 
 
-def test_corpus_quads_through_keyset_path():
-    """The key-cache kernel's batch of 4 signatures per lane (one inversion for
-    all four, R'_j staged): every corpus entry in a quad with three neighbours."""
+def test_corpus_through_keyset_path():
+    """The key-cache kernel's batch of 8 signatures per lane (one inversion for
+    all eight, R'_j staged): every corpus entry in a group of 8 with seven
+    neighbours, plus groups of 3 (the count is a kernel argument)."""
     d = np.load(os.path.join(GOLD, "ed25519_corpus.npz"))
     n = len(d["cat"])
 
@@ -145,15 +146,16 @@ def test_corpus_quads_through_keyset_path():
         o, ln = int(d["off"][i]), int(d["len"][i])
         return d["pk"][i].tobytes(), d["sig"][i].tobytes(), d["msg"][o:o + ln].tobytes()
 
-    for i in range(0, n, 4):
-        idx = [(i + k) % n for k in range(4)]
-        for mode, key in ((0, "strict"), (1, "batch_rule")):
-            want = tuple(bool(d[key][j]) for j in idx)
-            assert H.verify_cached4(mode, [entry(j) for j in idx]) == want, (i, mode)
-        # mixed mode (one launch for header + vote signatures): per-entry strictness
-        mask = (i // 4) % 16
-        want = tuple(bool(d["strict" if (mask >> k) & 1 else "batch_rule"][j]) for k, j in enumerate(idx))
-        assert H.verify_cached4(2, [entry(j) for j in idx], strict_mask=mask) == want, (i, "mixed", mask)
+    for g, step in ((8, 8), (3, 37)):
+        for i in range(0, n, step):
+            idx = [(i + k) % n for k in range(g)]
+            for mode, key in ((0, "strict"), (1, "batch_rule")):
+                want = tuple(bool(d[key][j]) for j in idx)
+                assert H.verify_cached_n(mode, [entry(j) for j in idx]) == want, (i, mode)
+            # mixed mode (one launch for header + vote signatures): per-entry strictness
+            mask = (i * 37 // step) % (1 << g)
+            want = tuple(bool(d["strict" if (mask >> k) & 1 else "batch_rule"][j]) for k, j in enumerate(idx))
+            assert H.verify_cached_n(2, [entry(j) for j in idx], strict_mask=mask) == want, (i, "mixed", mask)
 
 
 def test_sc_halfsize_properties():

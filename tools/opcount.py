@@ -41,11 +41,11 @@ def measure():
         out[name + "_fe_mul"] = mul
         out[name + "_fe_sq"] = sq
         out[name + "_mads"] = round(100 * mul + 55 * sq, 1)
-        # key-cache kernel: 4 signatures per lane, one inversion
+        # key-cache kernel: 8 signatures per lane (keyset_per_lane()), one inversion
         H.counts_reset()
-        for i in range(NPAIRS // 2):
-            q = [(sigs[4 * i + k][0], sigs[4 * i + k][1], msg) for k in range(4)]
-            assert H.verify_cached4(mode, q) == (True,) * 4
+        for i in range(NPAIRS // 4):
+            q = [(sigs[8 * i + k][0], sigs[8 * i + k][1], msg) for k in range(8)]
+            assert H.verify_cached_n(mode, q) == (True,) * 8
         mul, sq = H.counts()
         mul, sq = mul / (2 * NPAIRS), sq / (2 * NPAIRS)
         out[name + "_keyset_fe_mul"] = mul
@@ -57,9 +57,10 @@ def measure():
     mul, sq = H.counts()
     out["sign_fe_mul"], out["sign_fe_sq"], out["sign_mads"] = mul, sq, 100 * mul + 55 * sq
     out["verify_sha512_blocks_512B_msg"] = (64 + 512 + 17 + 127) // 128
-    out["note"] = ("host-compiled device code, two signatures per lane as the kernels run them, averaged "
-                   "over %d pairs (per-signature = pair / 2); fe_mul = 100 v_mad_u64_u32, fe_sq = 55; "
-                   "table builds (wide combs) excluded" % NPAIRS)
+    out["note"] = ("host-compiled device code as the kernels run it (verify: two signatures per lane, "
+                   "averaged over %d pairs, per-signature = pair / 2; key cache: 8 per lane sharing one "
+                   "inversion); B comb %d bits, key combs %d bits; fe_mul = 100 v_mad_u64_u32, fe_sq = 55; "
+                   "table builds (wide combs) excluded" % (NPAIRS, H.bcomb_bits(), 20))
     return out
 
 
