@@ -48,6 +48,7 @@ MAD_PEAK_TS = 256 * 4 * 64 * 2.4e9 / 4 / 1e12  # v_mad_u64_u32: 4 cycles per wav
 MAD_MEASURED_TS = 32.80  # profiles/r01_alu_rate.txt (tools/microbench): 4.80 cycles per wave64 per SIMD
 HBM_PEAK_GBS = 8000.0
 PMC_PROFILE = os.path.join("r02", "pmc_verify_sha.json")  # tools/profile_round.sh + tools/pmc_summarize.py
+PMC_KEYSET_PROFILE = os.path.join("r02", "pmc_keyset.json")  # cfg3 key-cache launch, 8 signatures per lane
 PMC_N = 1_000_000  # signatures per launch in that profile (the default config-2 run)
 SODIUM = "/opt/conda/lib/libsodium.so.23"
 
@@ -627,7 +628,9 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
         m_len[:V] = v_len[perm]
         perm = perm.cpu().numpy()
 
-    def step(cached):
+    kev = []  # (start, end) events around the key-cache launch of each timed step
+
+    def step(cached, timed=False):
         be.dev_sha512(0, sp, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, hd2.data_ptr())
         be.dev_sha512(0, sp, cpre.data_ptr(), c_off.data_ptr(), c_len.data_ptr(), G, cd2.data_ptr())
         if cached and not fused:   # A/B reference: the header and vote launches separately
@@ -637,8 +640,13 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                           v_off.data_ptr(), v_len.data_ptr(), V, vbits.data_ptr())
             be.dev_group_and(0, sp, first.data_ptr(), cnt.data_ptr(), G, vbits.data_ptr(), gbits.data_ptr())
         elif cached:
+            if timed:
+                kev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                kev[-1][0].record(stream)
             ks.dev_verify(0, sp, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), msgbuf.data_ptr(),
                           m_off.data_ptr(), m_len.data_ptr(), V + G, mbits.data_ptr())
+            if timed:
+                kev[-1][1].record(stream)
             be.dev_group_and(0, sp, first.data_ptr(), cnt.data_ptr(), G, mbits.data_ptr(), gbits.data_ptr())
         else:
             be.dev_verify(0, sp, ntcrypto.NT_MODE_STRICT, tmp_pk.data_ptr(), hsig.data_ptr(), ids.data_ptr(),
@@ -672,7 +680,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
         t0 = time.perf_counter()
         ev0.record(stream)
         for _ in range(steps):
-            step(cached)
+            step(cached, timed=True)
         ev1.record(stream)
         barrier()
         wall = max_over_ranks(time.perf_counter() - t0)
@@ -683,6 +691,8 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                     "sig_verifies_per_s": round(G_total * (quorum + 1) * steps / wall, 1),
                     "ms_per_step": round(wall * 1e3 / steps, 3), "gpu_ms_per_step": round(kms, 3),
                     "mismatches_vs_expected": mism}
+        if cached and fused and kev:
+            out[key]["roofline"] = keyset_roofline(np.mean([a.elapsed_time(b) for a, b in kev]), V + G)
     ks.close()
     if world == 1 and not getattr(args, "no_cpu", False):
         out["cpu_baseline"] = cert_cpu_baseline(args, hdr, hlen, ids, tmp_pk, hsig, cpre, vpk, vsig, quorum, expect)
@@ -692,11 +702,39 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
             "scaling": "strong (certificates sharded over ranks)",
             "key_cache": {"comb_bits": ks_bits, "gb_per_device": round(ks_bytes / 1e9, 2),
                           "build_s": round(ks_build_s, 3),
-                          "note": "per-key wide combs of -A (13 comb additions per [k]A at 20 bits), built once "
+                          "note": "per-key wide combs of -A (13 comb additions per [k]A at 20 bits; [s]B: 11 "
+                                  "additions from the device's 24-bit comb of B), built once "
                                   "per committee on every device; not in the timed region",
                           "launches": "per step: 2 SHA-512 (header ids, certificate digests), 1 NT_MODE_MIXED key-cache "
                                       "verify (67 votes cofactorless + the header signature strict), 1 group AND"},
             **out}
+
+
+def keyset_roofline(kernel_ms, nsig):
+    """The config-3 key-cache launch (k_ed25519_verify_keyset, NT_MODE_MIXED) against
+    the same v_mad_u64_u32 issue peak as the headline kernel; the instruction
+    count, issue share and HBM traffic come from the committed PMC profile."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "opcount.json")) as f:
+            mads = float(json.load(f)["verify_cofactorless_keyset_mads"])
+    except Exception:
+        return None
+    achieved = mads * nsig / (kernel_ms * 1e-3) / 1e12
+    pk = (load_profile(PMC_KEYSET_PROFILE) or {}).get("kernels", {}).get("verify_keyset", {})
+    pkl = pk.get("per_launch", {})
+    grid = pk.get("grid")
+    return {"bound": "valu", "kernel": "k_ed25519_verify_keyset<mixed>", "kernel_ms": round(kernel_ms, 3),
+            "signatures_per_launch": nsig, "mads_per_signature": mads,
+            "achieved": round(achieved, 3), "peak": round(MAD_PEAK_TS, 2), "unit": "Tmad/s",
+            "frac": round(achieved / MAD_PEAK_TS, 4),
+            "frac_vs_measured_mad_rate": round(achieved / MAD_MEASURED_TS, 4),
+            "valu_instr_per_signature": (round(pkl["SQ_INSTS_VALU"] * 64 / (grid * 8)) if grid and "SQ_INSTS_VALU" in pkl
+                                         else None),
+            "valu_issue_share": round(pk["valu_issue_share_4cyc"], 3) if "valu_issue_share_4cyc" in pk else None,
+            "traffic": pk.get("hbm_bytes_per_launch"),
+            "traffic_note": "HBM bytes per launch (profiles/%s, FETCH_SIZE*2 + WRITE_SIZE): 24 random 128-B comb "
+                            "lines (3 KB) + ~250 B of inputs + the 160-B stash round trip per signature"
+                            % PMC_KEYSET_PROFILE}
 
 
 def bench_latency(be, pk_h, sig_h, msg_h, L):

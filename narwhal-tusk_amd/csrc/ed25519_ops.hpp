@@ -59,11 +59,11 @@ constexpr int kWChunk = 64;   // consecutive entries built by one thread
 #endif
 // comb of the base point B (one per device): 24 bits by measurement
 constexpr int kBCombBits = NT_BCOMB_BITS;
-static_assert(kBCombBits == 16 || kBCombBits == 20 || kBCombBits == 22 || kBCombBits == 24, "B comb width must be a built width");
+static_assert(kBCombBits == 16 || kBCombBits == 20 || kBCombBits == 22 || kBCombBits == 24 || kBCombBits == 26, "B comb width must be a built width");
 
 template <int W>
 struct CombGeom {
-  static_assert(W >= 12 && W <= 24, "comb digit width");
+  static_assert(W >= 12 && W <= 26, "comb digit width");
   static constexpr int kPos = (254 + W - 1) / W;          // signed digits of a 253-bit scalar
   static constexpr int kEntries = (1 << (W - 1)) + 1;     // |digit| in 0..2^(W-1)
   static constexpr int kChunks = (1 << (W - 1)) / kWChunk;  // chunks per position: entries 1..2^(W-1)

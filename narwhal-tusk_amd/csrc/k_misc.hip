@@ -379,9 +379,13 @@ hipError_t launch_wcomb_build(int bits, const uint32_t* d_enc, uint32_t nkeys, i
     case kKeyCombWide: return wcomb_build<kKeyCombWide>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
     case kKeyCombMid: return wcomb_build<kKeyCombMid>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
     case 24: return wcomb_build<24>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);  // B only
-    case 22:  // B only, -DNT_BCOMB_BITS=22 builds (A/B)
+    case 22:  // B only, -DNT_BCOMB_BITS=22 / 26 builds (A/B)
       if constexpr (kBCombBits == 22)
         return wcomb_build<22>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
+      return hipErrorInvalidValue;
+    case 26:
+      if constexpr (kBCombBits == 26)
+        return wcomb_build<26>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
       return hipErrorInvalidValue;
     case kKeyCombNarrow:
       return wcomb_build<kKeyCombNarrow>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
@@ -571,6 +575,7 @@ static size_t comb_size(int bits, int what) {
          : bits == kKeyCombNarrow ? comb_size<kKeyCombNarrow>(what)
          : bits == 24             ? comb_size<24>(what)
          : bits == 22             ? comb_size<22>(what)
+         : bits == 26             ? comb_size<26>(what)
                                   : 0;
 }
 size_t wcomb_bytes_per_key(int bits) { return comb_size(bits, 0); }
