@@ -289,10 +289,10 @@ def main():
                 "traffic": pv.get("hbm_bytes_per_launch"),
                 "traffic_note": ("HBM bytes per launch from rocprofv3 FETCH_SIZE*2 + WRITE_SIZE (profiles/%s, "
                                  "same kernel build, separate --pmc passes; the config-2 launch, grouped by grid size). "
-                                 "Algorithmic minimum ~2.3 KB/verify (608 B of input + 13 comb lines of B); the rest "
-                                 "(~13.4 KB/verify) is this kernel's own per-lane [j]A/[j]R table workspace (2,880 B "
-                                 "written, ~10.5 KB read), i.e. ~9.6x the minimum -- 2.1 TB/s, not the limiter of an "
-                                 "issue-bound kernel" % PMC_PROFILE)
+                                 "Algorithmic minimum ~2.0 KB/verify (608 B of input + 11 comb lines of B); the rest "
+                                 "(~13.4 KB/verify of the ~21.9 KB measured, plus line over-fetch) is this kernel's own "
+                                 "per-lane [j]A/[j]R table workspace (2,880 B written, ~10.5 KB read), ~11x the "
+                                 "minimum in all -- 2.1 TB/s, not the limiter of an issue-bound kernel" % PMC_PROFILE)
                 if pv else None,
                 "kernel": "k_ed25519_verify<strict>", "kernel_ms": round(kernel_ms, 3),
                 "mads_per_verify": mads,
