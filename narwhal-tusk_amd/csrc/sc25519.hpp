@@ -186,6 +186,9 @@ NT_HD NT_INLINE void sc_recode_w16(uint32_t out[8], const uint32_t s[8]) {
 // bits is used.  Anything unexpected (step cap, > 250 bits) falls back to the
 // trivial vector (k, 1).  Returns max(bitlen|u|, bitlen v) (never an
 // underestimate).  Per-lane loop lengths differ (~73 steps on average).
+// Down to r1 ~ 2^136 the steps run in Lehmer batches (lat_lehmer_batch:
+// ~20 quotients per fp64 run, one matrix update of the multiword state),
+// landing on the same remainder pairs; the one-step loop finishes.
 // ---------------------------------------------------------------------------
 template <int N>
 NT_HD NT_INLINE double bn_to_f64(const uint32_t* a) {
@@ -248,44 +251,214 @@ NT_HD NT_INLINE uint32_t lat_quot(double d0, double d1) {
 constexpr int kLatMaxSteps = 600;
 constexpr double kLatStop = 0x1.6a09e667f3bcdp+127;  // 2^127.5
 
-NT_HD NT_INLINE int sc_halfsize(uint32_t u[8], uint32_t& uneg, uint32_t v[8], const uint32_t k[8]) {
+// n-word helpers of the Lehmer batches
+// out[0..N] = a * m
+template <int N>
+NT_HD NT_INLINE void bn_mul1(uint32_t* out, const uint32_t* a, uint32_t m) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint64_t p = (uint64_t)m * a[i] + c;
+    out[i] = (uint32_t)p;
+    c = p >> 32;
+  }
+  out[N] = (uint32_t)c;
+}
+// out = a - b over N words; returns the borrow
+template <int N>
+NT_HD NT_INLINE uint32_t bn_sub(uint32_t* out, const uint32_t* a, const uint32_t* b) {
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint64_t t = (uint64_t)a[i] - b[i] - br;
+    out[i] = (uint32_t)t;
+    br = (uint32_t)(t >> 63);
+  }
+  return br;
+}
+// a += b over N words; returns the carry
+template <int N>
+NT_HD NT_INLINE uint32_t bn_add(uint32_t* a, const uint32_t* b) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    c += (uint64_t)a[i] + b[i];
+    a[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return (uint32_t)c;
+}
+
+// Remainder-sequence state: r0 > r1 >= 0 (8 words), |t0|, |t1| (4 words, of
+// opposite signs, t1neg = sign of t1), fp64 images d0, d1, steps taken.
+struct LatState {
   uint32_t r0[8], r1[8], t0[4], t1[4];
+  uint32_t t1neg;
+  double d0, d1;
+  int steps;
+};
+
+// One exact step: r0 -= q r1 with q = floor(d0 / d1) rounded down (a short
+// quotient is a partial step), swap when r0 < r1.
+NT_HD NT_INLINE void lat_exact_step(LatState& S) {
+  const uint32_t q = lat_quot(S.d0, S.d1);
+  bn_submul1<8>(S.r0, S.r1, q);
+  bn_addmul1<4>(S.t0, S.t1, q);
+  S.d0 = bn_to_f64<8>(S.r0);
+  const uint32_t sw = bn_lt<8>(S.r0, S.r1);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    r0[i] = kSc8L[i];
-    r1[i] = k[i];
+    const uint32_t a = S.r0[i], b = S.r1[i];
+    S.r0[i] = sw ? b : a;
+    S.r1[i] = sw ? a : b;
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) t0[i] = t1[i] = 0;
-  t1[0] = 1;
-  uint32_t t1neg = 0;
-  double d0 = bn_to_f64<8>(r0), d1 = bn_to_f64<8>(r1);
-  int steps = 0;
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t a = S.t0[i], b = S.t1[i];
+    S.t0[i] = sw ? b : a;
+    S.t1[i] = sw ? a : b;
+  }
+  const double e0 = S.d0;
+  S.d0 = sw ? S.d1 : S.d0;
+  S.d1 = sw ? e0 : S.d1;
+  S.t1neg ^= sw;
+  ++S.steps;
+}
+
+// Lehmer batch: Euclid on the leading 53 bits of (r0, r1) in fp64, then ONE
+// 2x2 cofactor matrix applied to the 256-bit remainders and the t's, instead
+// of a multiword update per quotient.  a = the 53-bit mantissa of d0 (r0 / 2^sh),
+// b = floor(d1 / 2^sh); both are within E = 8 of the true r / 2^sh (seven fma
+// roundings in bn_to_f64 + the floor).  After j steps with cofactor magnitudes
+// (x, y) a truncated remainder differs from the exact one (/ 2^sh) by at most
+// E (x + y), so a step is accepted only while its new remainder r exceeds that
+// bound and b - r exceeds the bound of both rows: then the exact remainders stay
+// positive and ordered, i.e. every accepted quotient IS the exact Euclid
+// quotient and the batch lands on the same remainder pair the one-step loop
+// visits.  Steps stop above 2^132 (the one-step loop finishes the last few).
+// The applied state is re-validated (r0' > r1' >= 0, |t| in 4 words); an
+// empty or invalid batch falls back to one exact step.
+constexpr double kLehmerStop = 0x1p136;  // batches while r1 >= 2^136
+constexpr int kLehmerMaxInner = 48;      // > the 37 all-ones quotients of 26 bits
+NT_HD NT_INLINE void lat_lehmer_batch(LatState& S) {
+  int e;
+  frexp(S.d0, &e);
+  const int sh = e - 53;  // d0 in [2^(e-1), 2^e): d0 / 2^sh is an integer in [2^52, 2^53)
+  double a = ldexp(S.d0, -sh), b = floor(ldexp(S.d1, -sh));
+  const double thr = ldexp(1.0, 132 - sh);
+  double x0 = 1.0, y0 = 0.0, x1 = 0.0, y1 = 1.0;
+  int n = 0;
+#pragma unroll 1
+  for (int it = 0; it < kLehmerMaxInner; ++it) {
+    if (!(b >= 1.0)) break;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // v_rcp_f64 (~1 ulp) instead of the IEEE division sequence: an estimate off
+    // by more than the one correction below fails the acceptance test
+    double q = floor(a * __builtin_amdgcn_rcp(b));
+#else
+    double q = floor(a / b);
+#endif
+    double r = fma(-q, b, a);  // exact: every operand and product < 2^53
+    if (r < 0.0) {
+      q -= 1.0;
+      r += b;
+    } else if (r >= b) {
+      q += 1.0;
+      r -= b;
+    }
+    const double x2 = fma(q, x1, x0), y2 = fma(q, y1, y0);
+    if (!(r >= thr && r > 8.0 * (x2 + y2) && b - r > 8.0 * (x1 + y1 + x2 + y2))) break;
+    a = b;
+    b = r;
+    x0 = x1;
+    y0 = y1;
+    x1 = x2;
+    y1 = y2;
+    ++n;
+  }
+  // (cofactors < 2^26 here: r > 8 (x + y) with r < 2^53)
+  const uint32_t X0 = (uint32_t)x0, Y0 = (uint32_t)y0, X1 = (uint32_t)x1, Y1 = (uint32_t)y1;
+  const uint32_t odd = (uint32_t)n & 1u;
+  // remainder j of the batch = (-1)^j (x_j r0 - y_j r1): r0' is j = n, r1' is j = n + 1
+  uint32_t P[9], Q[9], A[9], B[9], n0[9], n1[9];
+  bn_mul1<8>(P, S.r0, X0);
+  bn_mul1<8>(Q, S.r1, Y0);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    A[i] = odd ? Q[i] : P[i];
+    B[i] = odd ? P[i] : Q[i];
+  }
+  uint32_t bad = bn_sub<9>(n0, A, B);
+  bn_mul1<8>(P, S.r0, X1);
+  bn_mul1<8>(Q, S.r1, Y1);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    A[i] = odd ? P[i] : Q[i];
+    B[i] = odd ? Q[i] : P[i];
+  }
+  bad |= bn_sub<9>(n1, A, B);
+  bad |= (n0[8] | n1[8]) != 0u;
+  bad |= bn_lt<8>(n1, n0) ^ 1u;
+  // |t_j| = x_j |t0| + y_j |t1| (t0, t1 of opposite signs)
+  uint32_t m0[5], m1[5], w[5];
+  bn_mul1<4>(m0, S.t0, X0);
+  bn_mul1<4>(w, S.t1, Y0);
+  bn_add<5>(m0, w);
+  bn_mul1<4>(m1, S.t0, X1);
+  bn_mul1<4>(w, S.t1, Y1);
+  bn_add<5>(m1, w);
+  bad |= (m0[4] | m1[4]) != 0u;
+  if (n == 0 || bad) {
+    lat_exact_step(S);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    S.r0[i] = n0[i];
+    S.r1[i] = n1[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    S.t0[i] = m0[i];
+    S.t1[i] = m1[i];
+  }
+  S.t1neg ^= odd;
+  S.d0 = bn_to_f64<8>(S.r0);
+  S.d1 = bn_to_f64<8>(S.r1);
+  S.steps += n;
+}
+
+// LEHMER = false: the one-step loop only (the reference the tests compare the
+// batched reduction with; the kernels use LEHMER = true).
+template <bool LEHMER>
+NT_HD NT_INLINE int sc_halfsize_t(uint32_t u[8], uint32_t& uneg, uint32_t v[8], const uint32_t k[8]) {
+  LatState S;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    S.r0[i] = kSc8L[i];
+    S.r1[i] = k[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) S.t0[i] = S.t1[i] = 0;
+  S.t1[0] = 1;
+  S.t1neg = 0;
+  S.d0 = bn_to_f64<8>(S.r0);
+  S.d1 = bn_to_f64<8>(S.r1);
+  S.steps = 0;
+  if (LEHMER) {
+#pragma unroll 1
+    while (S.d1 >= kLehmerStop && S.steps < kLatMaxSteps) lat_lehmer_batch(S);
+  }
   // Inside the loop r1 >= 2^127.5, so |t0|, |t1| <= 8L / r1 < 2^128: 4 words.
-  while (d1 >= kLatStop && steps < kLatMaxSteps) {
-    const uint32_t q = lat_quot(d0, d1);
-    bn_submul1<8>(r0, r1, q);
-    bn_addmul1<4>(t0, t1, q);
-    d0 = bn_to_f64<8>(r0);
-    const uint32_t sw = bn_lt<8>(r0, r1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t a = r0[i], b = r1[i];
-      r0[i] = sw ? b : a;
-      r1[i] = sw ? a : b;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t a = t0[i], b = t1[i];
-      t0[i] = sw ? b : a;
-      t1[i] = sw ? a : b;
-    }
-    const double e0 = d0;
-    d0 = sw ? d1 : d0;
-    d1 = sw ? e0 : d1;
-    t1neg ^= sw;
-    ++steps;
-  }
+#pragma unroll 1
+  while (S.d1 >= kLatStop && S.steps < kLatMaxSteps) lat_exact_step(S);
+  uint32_t(&r0)[8] = S.r0;
+  uint32_t(&r1)[8] = S.r1;
+  uint32_t(&t0)[4] = S.t0;
+  uint32_t(&t1)[4] = S.t1;
+  const uint32_t t1neg = S.t1neg;
+  const double d0 = S.d0, d1 = S.d1;
+  const int steps = S.steps;
   int bits;
   if (t1[0] & 1u) {
 #pragma unroll
@@ -334,6 +507,16 @@ NT_HD NT_INLINE int sc_halfsize(uint32_t u[8], uint32_t& uneg, uint32_t v[8], co
     bits = 253;
   }
   return bits;
+}
+NT_HD NT_INLINE int sc_halfsize(uint32_t u[8], uint32_t& uneg, uint32_t v[8], const uint32_t k[8]) {
+#ifdef NT_LAT_ONE_STEP  // A/B builds only
+  return sc_halfsize_t<false>(u, uneg, v, k);
+#else
+  return sc_halfsize_t<true>(u, uneg, v, k);
+#endif
+}
+NT_HD NT_INLINE int sc_halfsize_euclid(uint32_t u[8], uint32_t& uneg, uint32_t v[8], const uint32_t k[8]) {
+  return sc_halfsize_t<false>(u, uneg, v, k);
 }
 
 // (v * s) mod L for v, s < 2^256

@@ -127,6 +127,13 @@ def sc_halfsize(k: int):
     return (-uu if neg.value else uu), int.from_bytes(v.raw, "little"), bits
 
 
+def halfsize_disagree(ks):
+    """number of scalars (ints < 2^256) whose batched (Lehmer) and one-step
+    lattice reductions differ in (u, v, sign, bits)"""
+    buf = b"".join(k.to_bytes(32, "little") for k in ks)
+    return int(load().nth_halfsize_disagree(buf, len(ks)))
+
+
 def small_order(enc):
     """(decodes, [8]P == 0 by doublings, torsion-y compare) for a 32-byte encoding"""
     a, b = ctypes.c_int(0), ctypes.c_int(0)

@@ -181,6 +181,19 @@ int nth_sc_halfsize(const uint8_t* k32, uint8_t* u32, uint8_t* v32, int* uneg) {
   *uneg = (int)un;
   return bits;
 }
+// Batched (Lehmer) vs one-step lattice reduction on n scalars (32 bytes each):
+// the number whose (u, v, sign, bits) differ.
+int nth_halfsize_disagree(const uint8_t* ks, int n) {
+  int bad = 0;
+  for (int i = 0; i < n; ++i) {
+    uint32_t k[8], u0[8], v0[8], u1[8], v1[8], n0, n1;
+    words(k, ks + 32 * (size_t)i);
+    const int b0 = sc_halfsize(u0, n0, v0, k);
+    const int b1 = sc_halfsize_euclid(u1, n1, v1, k);
+    bad += (b0 != b1 || n0 != n1 || std::memcmp(u0, u1, 32) != 0 || std::memcmp(v0, v1, 32) != 0) ? 1 : 0;
+  }
+  return bad;
+}
 void nth_sha512(const uint8_t* msg, uint64_t len, uint8_t* out64) {
   uint64_t st[8];
   sha512_prefixed<0>(st, nullptr, msg, len);

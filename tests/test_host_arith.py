@@ -158,6 +158,26 @@ def test_corpus_through_keyset_path():
             assert H.verify_cached_n(2, [entry(j) for j in idx], strict_mask=mask) == want, (i, "mixed", mask)
 
 
+def test_sc_halfsize_lehmer_equals_one_step():
+    """The Lehmer-batched reduction the kernels run lands on exactly the
+    (u, v, sign, bits) of the one-step Euclid loop: random k < L, k near L,
+    near 2^252, small / power-of-two / Fibonacci-ratio scalars (all-ones
+    quotient runs) and huge partial quotients."""
+    rng = random.Random(1234)
+    ks = [rng.randrange(H.L) for _ in range(200_000)]
+    ks += [H.L - 1 - i for i in range(64)] + [(1 << 252) + i for i in range(64)] + [(1 << 252) - 1 - i for i in range(64)]
+    ks += [0, 1, 2, 3] + [1 << b for b in range(0, 253)] + [(1 << b) - 1 for b in range(1, 253)]
+    # k / 8L close to a ratio of consecutive Fibonacci numbers -> long runs of quotient 1
+    fa, fb = 1, 1
+    while fb < 1 << 126:
+        fa, fb = fb, fa + fb
+    ks += [(8 * H.L * fa // fb + d) % H.L for d in range(-32, 33)]
+    # huge first quotients: k tiny relative to 8L, and 8L / k just above an integer
+    ks += [(8 * H.L) // q + d for q in (3, 1 << 20, 1 << 31, (1 << 32) + 1, 1 << 40, 1 << 60) for d in range(-3, 4)]
+    ks = [k % H.L for k in ks]
+    assert H.halfsize_disagree(ks) == 0
+
+
 def test_sc_halfsize_properties():
     """Half-size scalars (sc25519.hpp): for every k < L the result satisfies
     u == v k (mod 8L), v odd, 0 < v < L, and bits >= bitlen(|u|), bitlen(v)
