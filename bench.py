@@ -466,7 +466,7 @@ def bench_sha_real(args, torch, dev, be, sp, stream, world, rank, barrier, max_o
 def sha_cpu_baseline(args, data, out, m, ml):
     """Config 4 on the host cores: the oracle's C SHA-512 (oracle/ntoracle.c, FIPS 180-4
     restatement of sha2's software compress) over a bounded sample of the same
-    messages, args.cpu_threads threads, median of 3 runs; digests compared with the GPU's."""
+    messages, args.cpu_threads threads, 1 warm-up + median of 5 runs; digests compared with the GPU's."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle
     orc = _oracle.load()
@@ -478,15 +478,15 @@ def sha_cpu_baseline(args, data, out, m, ml):
     t0 = time.perf_counter()
     orc.sha512_trunc32_many(host, offs[:1], lens[:1], nthreads=1)
     one = time.perf_counter() - t0
-    # repeat the sample until ~args.cpu_seconds of CPU work, in 3 timed runs (median)
+    # repeat the sample until ~args.cpu_seconds of CPU work per run; 1 warm-up + median of 5 runs
     reps = max(1, int(round(args.cpu_seconds / 3 / (k * one))))
-    times = []
-    for _ in range(3):
-        t0 = time.perf_counter()
+
+    def sha_run():
         for _ in range(reps):
-            dig = orc.sha512_trunc32_many(host, offs, lens, nthreads=th)
-        times.append((time.perf_counter() - t0) / reps)
-    dt = sorted(times)[1]
+            d = orc.sha512_trunc32_many(host, offs, lens, nthreads=th)
+        return d
+    dt, dig = timed_median(sha_run)
+    dt /= reps
     gpu = out[:k].cpu().numpy()
     agree = int((dig == gpu).all(axis=1).sum())
     # external comparator: OpenSSL's SHA-512 through hashlib (releases the GIL), th Python threads
@@ -497,20 +497,21 @@ def sha_cpu_baseline(args, data, out, m, ml):
     def work(t):
         for i in range(t, k, th):
             ext_dig[i] = hashlib.sha512(memoryview(host)[i * ml:(i + 1) * ml]).digest()[:32]
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        ts = [threading.Thread(target=work, args=(t,)) for t in range(th)]
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
-    edt = (time.perf_counter() - t0) / reps
+    def ext_run():
+        for _ in range(reps):
+            ts = [threading.Thread(target=work, args=(t,)) for t in range(th)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+    edt, _ = timed_median(ext_run)
+    edt /= reps
     eagree = sum(int(ext_dig[i] == gpu[i].tobytes()) for i in range(k))
     host = host_cpu()
     gbs = k * ml / dt / 1e9
     return {"value": round(gbs, 3), "unit": "GB/s (message bytes)", "cores": th, "kind": "port",
             "label": "FIPS 180-4 C restatement of sha2 0.9's software compress (oracle/sha512_ref.c)",
-            "sample": "first %d of the same %d-B cfg4 messages (%.0f MB) hashed %d times per run, median of 3 "
+            "sample": "first %d of the same %d-B cfg4 messages (%.0f MB) hashed %d times per run, 1 warm-up + median of 5 "
                       "runs (%.2f s wall each)" % (k, ml, k * ml / 1e6, reps, dt * reps),
             "host": host, "full_host_estimate": full_host(gbs, th, host),
             "single_thread_gbs": round(ml / one / 1e9, 3),
@@ -935,18 +936,14 @@ def cert_cpu_baseline(args, hdr, hlen, ids, hpk, hsig, cpre, vpk, vsig, quorum, 
     _, one = run(4, 1)
     per = one / 4
     sample = int(min(G, max(th * 8, args.cpu_seconds / per)))
-    times = []
-    for _ in range(3):
-        res, dt = run(sample, th)
-        times.append(dt)
-    dt = sorted(times)[1]
+    dt, (res, _) = timed_median(lambda: run(sample, th))
     agree = int((res.astype(bool) == expect[:sample]).sum())
     host = host_cpu()
     return {"value": round(sample / dt, 1), "unit": "certificates/s", "cores": th, "kind": "port",
             "label": "dalek-equivalent CPU restatement: Certificate::verify's 2 SHA-512 digests, verify_strict of "
                      "the header and dalek's randomized verify_batch of the %d votes (Straus / NAF-5 multiscalar)"
                      % quorum,
-            "sample": "first %d of the same cfg3 certificates, median of 3 runs (%.2f s wall each on %d threads)"
+            "sample": "first %d of the same cfg3 certificates, 1 warm-up + median of 5 runs (%.2f s wall each on %d threads)"
                       % (sample, dt, th),
             "single_thread_ms_per_certificate": round(per * 1e3, 3),
             "host": host, "full_host_estimate": full_host(sample / dt, th, host),
@@ -1070,17 +1067,14 @@ def cpu_baseline(args, pk_h, sig_h, msg_h, L, got):
     sample = int(min(len(pk_h), max(th * 64, args.cpu_seconds / per)))
     offs = (np.arange(sample, dtype=np.uint64) * L)
     lens = np.full(sample, L, np.uint64)
-    times = []
-    for _ in range(3):                    # median of 3 timed runs (SURVEY §8(d) procedure)
-        t0 = time.perf_counter()
-        res = orc.verify_strict_many(pk_h[:sample], sig_h[:sample], msg_h[:sample * L], offs, lens, nthreads=th)
-        times.append(time.perf_counter() - t0)
-    dt = sorted(times)[1]
+    # 1 warm-up + median of 5 timed runs (SURVEY §8(d) procedure)
+    dt, res = timed_median(lambda: orc.verify_strict_many(pk_h[:sample], sig_h[:sample], msg_h[:sample * L], offs,
+                                                          lens, nthreads=th))
     agree = int((res.astype(bool) == got[:sample]).sum())
     host = host_cpu()
     out = {"value": round(sample / dt, 1), "unit": "verifies/s", "cores": th, "kind": "port",
            "label": "dalek-equivalent CPU restatement (oracle/: curve25519-dalek u64-backend field arithmetic -- radix 2^51, dedicated square, lazy add -- and dalek's verify algorithms)",
-           "sample": "first %d of the same 1M cfg2 verifies, median of 3 runs (%.1f s wall each on %d threads)"
+           "sample": "first %d of the same 1M cfg2 verifies, 1 warm-up + median of 5 runs (%.1f s wall each on %d threads)"
                      % (sample, dt, th),
            "host": host, "full_host_estimate": full_host(sample / dt, th, host),
            "single_thread_us_per_verify": round(per * 1e6, 2),
@@ -1108,17 +1102,28 @@ def sodium_baseline(orc, pk_h, sig_h, msg_h, L, got, th, seconds):
     sample = int(min(len(pk_h), max(th * 64, seconds / per)))
     offs = np.arange(sample, dtype=np.uint64) * L
     lens = np.full(sample, L, np.uint64)
-    times = []
-    for _ in range(3):
-        t0 = time.perf_counter()
-        res = orc.sodium_verify_many(SODIUM, pk_h[:sample], sig_h[:sample], msg_h[:sample * L], offs, lens, th)
-        times.append(time.perf_counter() - t0)
-    dt = sorted(times)[1]
+    dt, res = timed_median(lambda: orc.sodium_verify_many(SODIUM, pk_h[:sample], sig_h[:sample], msg_h[:sample * L],
+                                                          offs, lens, th))
     agree = int((res.astype(bool) == got[:sample]).sum())
     return {"name": "libsodium 1.0.18 crypto_sign_verify_detached", "value": round(sample / dt, 1),
             "unit": "verifies/s", "cores": th, "kind": "external",
-            "sample": "first %d of the same cfg2 verifies, median of 3 runs (%.1f s wall each)" % (sample, dt),
+            "sample": "first %d of the same cfg2 verifies, 1 warm-up + median of 5 runs (%.1f s wall each)"
+                      % (sample, dt),
             "single_thread_us_per_verify": round(per * 1e6, 2), "verdicts_agree_with_gpu": "%d/%d" % (agree, sample)}
+
+
+def timed_median(fn, runs=5, warmup=1):
+    """SURVEY §8(d) procedure: `warmup` untimed calls, then the median wall time
+    of `runs` timed calls; returns (median seconds, result of the last call)."""
+    res = None
+    for _ in range(warmup):
+        res = fn()
+    times = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        res = fn()
+        times.append(time.perf_counter() - t0)
+    return sorted(times)[len(times) // 2], res
 
 
 def expand(label: bytes, n: int) -> bytes:
