@@ -293,6 +293,26 @@ def test_keyset_committee_random_vs_oracle(be, oracle):
     ks.close()
 
 
+def test_keyset_per_lane_counts():
+    """The key-cache kernel's per-lane signature count is a kernel argument
+    (keyset_per_lane(): 8 by default, NT_KEYSET_PER_LANE for A/B runs, read once
+    per process): counts 1, 3 and 5 -- partial waves, other stash strides, other
+    inversion batch sizes -- give the corpus verdicts in input order and in
+    key-grouped order (subprocesses: the variable is read at first use)."""
+    import json
+    import subprocess
+    import sys
+    probe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_keyset_per_lane_probe.py")
+    for m in (1, 3, 5):
+        env = dict(os.environ, NT_KEYSET_PER_LANE=str(m), NT_KEYSET_COMB_BITS="16")
+        r = subprocess.run([sys.executable, probe], env=env, capture_output=True, text=True, timeout=150)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+        assert res["per_lane"] == str(m)
+        bad = {k: v for k, v in res.items() if k.startswith("mismatches") and v}
+        assert not bad, (m, bad)
+
+
 @pytest.mark.gpu
 def test_keyset_key_grouped_order(be, corpus, monkeypatch):
     """Key-cache launches of >= 65,536 signatures verify in key-grouped order
