@@ -5,7 +5,7 @@
 #   3. PMC passes for the cfg3 key-cache launch
 # Usage: bash tools/profile_round.sh <tag>
 set -euo pipefail
-TAG=${1:-r01}
+TAG=${1:-r02c}
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
