@@ -1027,7 +1027,10 @@ def bench_ingest(args, be, world, rank, local, max_over_ranks, barrier):
         wall1 = max_over_ranks(time.perf_counter() - t0)
         phases = {k: round(v * 1e3, 2) for k, v in N.Core.last_stats().items()}
         # two chunks in flight: host decode/checks of one overlap the other's launches
-        chunk = max(1, (G + 3) // 4)
+        # 2 chunks (one per pipeline) measured best: 4 / 8 chunks pay the per-call
+        # overheads more often (profiles/r02/ab_ingest/)
+        nch = int(os.environ.get("NT_BENCH_INGEST_CHUNKS", "2"))
+        chunk = max(1, (G + nch - 1) // nch)
         core.ingest_pipelined(data, off, ln, args.ingest_threads, chunk)
         barrier()
         t0 = time.perf_counter()
@@ -1048,7 +1051,7 @@ def bench_ingest(args, be, world, rank, local, max_over_ranks, barrier):
             "decode_threads": args.ingest_threads, "wire_bytes_per_step": int(G * wlen),
             "phase_ms_last_step": phases,
             "note": "host decode into SoA + reference-order checks + 1 SHA-512, 1 verify_strict, 1 verify_batch "
-                    "launch (key cache) per chunk, 4 chunks with 2 in flight; PCIe-inclusive",
+                    "launch (key cache) per chunk, %d chunks on 2 pipelines; PCIe-inclusive" % nch,
             "mismatches_vs_expected": mism}
 
 
