@@ -174,7 +174,11 @@ void nt_host_free(void *p);
 int nt_dev_sha512_trunc32(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_data,
                           const uint64_t *d_off, const uint64_t *d_len, uint64_t n,
                           uint8_t *d_out32);
-/* d_out_words: ceil(n/64) little-endian 64-bit bitmap words. */
+/* d_out_words: ceil(n/64) little-endian 64-bit bitmap words.  Successive calls
+ * alternate between the device entry's two [k]A workspaces (each ordered by
+ * its own event), so batches enqueued back to back on two different streams
+ * overlap: the next batch's waves fill the SIMDs the previous batch's last
+ * round leaves idle.  Calls on one stream run in stream order. */
 int nt_dev_ed25519_verify(nt_ctx *ctx, int dev, void *stream, int mode, const uint8_t *d_pk32,
                           const uint8_t *d_sig64, const uint8_t *d_msg, const uint64_t *d_off,
                           const uint64_t *d_len, uint64_t n, uint64_t *d_out_words);

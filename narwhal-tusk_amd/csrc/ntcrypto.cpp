@@ -112,6 +112,7 @@ struct Device {
   hipEvent_t join2 = nullptr, ws2_done = nullptr;
   DevBuf ws2, stash2, sort2;
   std::mutex mu;
+  uint64_t dev_calls = 0;  // device-API verify calls (workspace alternation), under mu
   DevBuf d[B_NBUF];
   HostBuf h[B_NBUF];
   // Extra execution slots of the same device entry (NT_SLOTS, default 2 in
@@ -248,7 +249,7 @@ struct Device {
                    const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out) {
     if (!(c & 1)) return verify(mode, pk, sig, msg, off, len, n, out, stream) == hipSuccess ? NT_OK : NT_EHIP;
     const uint64_t blocks = nt::verify_grid(n, ws_slots);
-    const int rc = ws2.ensure(nt::ws_bytes_per_slot() * std::max<uint64_t>(blocks, 1));
+    const int rc = grow_ws2(blocks);
     if (rc != NT_OK) return rc;
     if (hipStreamWaitEvent(stream2, ws2_done, 0) != hipSuccess ||
         nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, ws2.p, (uint32_t)std::max<uint64_t>(blocks, 1),
@@ -269,6 +270,31 @@ struct Device {
     if (launch() != hipSuccess) return NT_EHIP;
     if (shared && hipEventRecord(stash_done, s) != hipSuccess) return NT_EHIP;
     return NT_OK;
+  }
+
+  // ws2 holds >= blocks workspace slots; a grown buffer is freed only after its
+  // last user (the kernel that recorded ws2_done) has finished
+  int grow_ws2(uint64_t blocks) {
+    const size_t need = nt::ws_bytes_per_slot() * std::max<uint64_t>(blocks, 1);
+    if (need <= ws2.cap) return NT_OK;
+    if (ws2.p && hipEventSynchronize(ws2_done) != hipSuccess) return NT_EHIP;
+    return ws2.ensure(need);
+  }
+
+  // Device-API verify (nt_dev_ed25519_verify): successive calls alternate between
+  // the two workspaces, each ordered by its own event, so back-to-back batches
+  // issued on two caller streams overlap -- the waves of the next batch fill the
+  // SIMDs the previous batch's last round leaves idle.  Calls on one stream stay
+  // in stream order.  (Caller holds mu.)
+  hipError_t verify_dev(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+                        const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out, hipStream_t s) {
+    if ((dev_calls++ & 1u) == 0) return verify(mode, pk, sig, msg, off, len, n, out, s);
+    if (grow_ws2(ws_slots) != NT_OK) return hipErrorOutOfMemory;
+    hipError_t e = hipStreamWaitEvent(s, ws2_done, 0);
+    if (e != hipSuccess) return e;
+    e = nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, ws2.p, ws_slots, out, s);
+    if (e != hipSuccess) return e;
+    return hipEventRecord(ws2_done, s);
   }
 
   // verify launch that shares the workspace: wait for the previous user, then mark
@@ -1311,9 +1337,9 @@ int nt_dev_ed25519_verify(nt_ctx* ctx, int dev, void* stream, int mode, const ui
   if (!dv || (mode != NT_MODE_STRICT && mode != NT_MODE_COFACTORLESS)) return NT_EINVAL;
   NT_TRY(hipSetDevice(dv->ordinal));
   hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
-  // the [k]A workspace is per device: serialize launches that use it
+  // the [k]A workspaces are per device: launches that use one are ordered by its event
   std::lock_guard<std::mutex> lk(dv->mu);
-  NT_TRY(dv->verify(mode, d_pk32, d_sig64, d_msg, d_off, d_len, n, d_out_words, s));
+  NT_TRY(dv->verify_dev(mode, d_pk32, d_sig64, d_msg, d_off, d_len, n, d_out_words, s));
   return NT_OK;
 }
 
