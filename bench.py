@@ -244,15 +244,15 @@ def main():
     sig.copy_(torch.from_numpy(sig_h))
     msgs.copy_(torch.from_numpy(msg_h))
     words = (n + 63) // 64
-    # Consecutive steps (independent 1M batches) alternate between two streams,
-    # the way a verifier fed a stream of batches runs: nt_dev_ed25519_verify
-    # alternates its two workspaces, so step i+1's waves fill the SIMDs step i's
-    # last round leaves idle.  Every step still verifies its whole batch; each
-    # step writes its own verdict buffer and both are checked.  NT_BENCH_STREAMS=1:
-    # one stream, launches strictly back to back.
-    nstreams = 2 if os.environ.get("NT_BENCH_STREAMS", "2") != "1" else 1
-    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nstreams - 1)]
-    outs = [torch.zeros(words, dtype=torch.int64, device=dev) for _ in range(nstreams)]
+    # The headline: launches strictly back to back on one stream.  Reported
+    # beside it ("pipelined_two_streams"): consecutive steps (independent 1M
+    # batches) alternating between two streams, the way a verifier fed a stream
+    # of batches runs -- nt_dev_ed25519_verify alternates its two workspaces, so
+    # step i+1's waves may fill the SIMDs step i's last round leaves idle.
+    # NT_BENCH_STREAMS=2 makes that mode the headline (A/B).
+    nstreams = 2 if os.environ.get("NT_BENCH_STREAMS", "1") == "2" else 1
+    streams = [stream, torch.cuda.Stream(dev)]
+    outs = [torch.zeros(words, dtype=torch.int64, device=dev) for _ in range(2)]
     out = outs[0]
     lev = []  # per-launch (start, end) events: each launch's own duration (what rocprof reports)
 
@@ -273,11 +273,11 @@ def main():
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for st in streams[1:]:
+    for st in streams[1:nstreams]:
         st.wait_event(ev0)
     for i in range(args.steps):
         step(i, timed=True)
-    for st in streams[1:]:
+    for st in streams[1:nstreams]:
         j = torch.cuda.Event()
         j.record(st)
         stream.wait_event(j)
@@ -338,6 +338,37 @@ def main():
             "roofline": roofline,
             "parity": {"mismatches_vs_expected": mism, "checked": n * world},
             "input_gen_s": round(gen_s, 3)}
+    line["streams"] = nstreams
+
+    # --------------- the same K batches with consecutive steps on alternating streams
+    if nstreams == 1:
+        barrier()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        streams[1].wait_event(e0)
+        for i in range(args.steps):
+            st = streams[i % 2]
+            be.dev_verify(0, st.cuda_stream, ntcrypto.NT_MODE_STRICT, pk.data_ptr(), sig.data_ptr(),
+                          msgs.data_ptr(), off.data_ptr(), ln.data_ptr(), n, outs[i % 2].data_ptr())
+        j = torch.cuda.Event()
+        j.record(streams[1])
+        stream.wait_event(j)
+        e1.record(stream)
+        barrier()
+        pwall = max_over_ranks(time.perf_counter() - t0)
+        pm = 0
+        for o in outs[:min(2, args.steps)]:
+            g2 = np.unpackbits(o.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+            pm += int((g2 != expect).sum())
+        line["pipelined_two_streams"] = {
+            "value": round(n * world * args.steps / pwall, 1), "ms_per_step": round(pwall * 1e3 / args.steps, 3),
+            "gpu_ms_per_step": round(e0.elapsed_time(e1) / args.steps, 3),
+            "mismatches_vs_expected": int(max_over_ranks(pm)),
+            "note": "not the headline: the same K 1M-verify steps with consecutive steps on two streams "
+                    "(nt_dev_ed25519_verify alternates its two workspaces), so a step's first waves may run "
+                    "in the previous step's last round"}
 
     # ------------------------------------------- same cfg2 batch through the host entry point
     # (caller buffers in ordinary host memory: PCIe-inclusive, never `value`)
@@ -625,21 +656,32 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
     first = torch.arange(G, dtype=torch.int64, device=dev) * quorum
     cnt = torch.full((G,), quorum, dtype=torch.int32, device=dev)
     hkey = author.to(torch.int32).contiguous()
-    hd2 = torch.empty((G, 32), dtype=torch.uint8, device=dev)
-    # one message buffer for the fused key-cache launch: certificate digests, then header ids
-    msgbuf = torch.empty((2 * G, 32), dtype=torch.uint8, device=dev)
-    msgbuf[G:] = ids
-    cd2 = msgbuf[:G]
-    hbits = torch.zeros(((G + 63) // 64,), dtype=torch.int64, device=dev)
-    vbits = torch.zeros(((V + 63) // 64 + 1,), dtype=torch.int64, device=dev)
-    gbits = torch.zeros(((G + 63) // 64,), dtype=torch.int64, device=dev)
+    # Consecutive steps (independent certificate batches) alternate between two
+    # streams, each with its own digest / verdict buffers, for the fused key-cache
+    # path (the device API alternates its two stashes, so the launches are
+    # independent); NT_BENCH_STREAMS=1: one stream.  The uncached reference runs
+    # on one stream.
+    nst = 2 if os.environ.get("NT_BENCH_STREAMS", "2") != "1" else 1
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nst - 1)]
+
+    def make_bufs():
+        b = {"hd2": torch.empty((G, 32), dtype=torch.uint8, device=dev),
+             # one message buffer for the fused key-cache launch: certificate digests, then header ids
+             "msgbuf": torch.empty((2 * G, 32), dtype=torch.uint8, device=dev),
+             "hbits": torch.zeros(((G + 63) // 64,), dtype=torch.int64, device=dev),
+             "vbits": torch.zeros(((V + 63) // 64 + 1,), dtype=torch.int64, device=dev),
+             "gbits": torch.zeros(((G + 63) // 64,), dtype=torch.int64, device=dev),
+             "mbits": torch.zeros(((V + G + 63) // 64 + 1,), dtype=torch.int64, device=dev)}
+        b["msgbuf"][G:] = ids
+        b["cd2"] = b["msgbuf"][:G]
+        return b
+    bufs = [make_bufs() for _ in range(nst)]
     # NT_MODE_MIXED inputs: V vote signatures (cofactorless), then G header signatures
     # (strict: key index with bit 31 set) -- Certificate::verify's two checks in one launch
     mkey = torch.cat([vkey, hkey + torch.iinfo(torch.int32).min]).contiguous()
     msig = torch.cat([vsig, hsig]).contiguous()
     m_off = torch.cat([v_off, G * 32 + i_off]).contiguous()
     m_len = torch.cat([v_len, i_len]).contiguous()
-    mbits = torch.zeros(((V + G + 63) // 64 + 1,), dtype=torch.int64, device=dev)
 
     fused = os.environ.get("NT_BENCH_FUSED", "1") != "0"
     # layout experiment (A/B only): the fused launch sees the votes grouped by
@@ -656,69 +698,89 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
 
     kev = []  # (start, end) events around the key-cache launch of each timed step
 
-    def step(cached, timed=False):
-        be.dev_sha512(0, sp, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, hd2.data_ptr())
-        be.dev_sha512(0, sp, cpre.data_ptr(), c_off.data_ptr(), c_len.data_ptr(), G, cd2.data_ptr())
+    mode_streams = {True: nst, False: 1}  # streams of the cached / uncached runs
+
+    def slots(cached):
+        return mode_streams[cached] if cached and fused else 1
+
+    def step(cached, i, timed=False):
+        k = i % slots(cached)
+        st = streams[k]
+        sq = st.cuda_stream
+        b = bufs[k]
+        be.dev_sha512(0, sq, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, b["hd2"].data_ptr())
+        be.dev_sha512(0, sq, cpre.data_ptr(), c_off.data_ptr(), c_len.data_ptr(), G, b["cd2"].data_ptr())
         if cached and not fused:   # A/B reference: the header and vote launches separately
-            ks.dev_verify(0, sp, ntcrypto.NT_MODE_STRICT, hkey.data_ptr(), hsig.data_ptr(), ids.data_ptr(),
-                          i_off.data_ptr(), i_len.data_ptr(), G, hbits.data_ptr())
-            ks.dev_verify(0, sp, ntcrypto.NT_MODE_COFACTORLESS, vkey.data_ptr(), vsig.data_ptr(), cd2.data_ptr(),
-                          v_off.data_ptr(), v_len.data_ptr(), V, vbits.data_ptr())
-            be.dev_group_and(0, sp, first.data_ptr(), cnt.data_ptr(), G, vbits.data_ptr(), gbits.data_ptr())
+            ks.dev_verify(0, sq, ntcrypto.NT_MODE_STRICT, hkey.data_ptr(), hsig.data_ptr(), ids.data_ptr(),
+                          i_off.data_ptr(), i_len.data_ptr(), G, b["hbits"].data_ptr())
+            ks.dev_verify(0, sq, ntcrypto.NT_MODE_COFACTORLESS, vkey.data_ptr(), vsig.data_ptr(), b["cd2"].data_ptr(),
+                          v_off.data_ptr(), v_len.data_ptr(), V, b["vbits"].data_ptr())
+            be.dev_group_and(0, sq, first.data_ptr(), cnt.data_ptr(), G, b["vbits"].data_ptr(), b["gbits"].data_ptr())
         elif cached:
             if timed:
                 kev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
-                kev[-1][0].record(stream)
-            ks.dev_verify(0, sp, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), msgbuf.data_ptr(),
-                          m_off.data_ptr(), m_len.data_ptr(), V + G, mbits.data_ptr())
+                kev[-1][0].record(st)
+            ks.dev_verify(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(),
+                          m_off.data_ptr(), m_len.data_ptr(), V + G, b["mbits"].data_ptr())
             if timed:
-                kev[-1][1].record(stream)
-            be.dev_group_and(0, sp, first.data_ptr(), cnt.data_ptr(), G, mbits.data_ptr(), gbits.data_ptr())
+                kev[-1][1].record(st)
+            be.dev_group_and(0, sq, first.data_ptr(), cnt.data_ptr(), G, b["mbits"].data_ptr(), b["gbits"].data_ptr())
         else:
-            be.dev_verify(0, sp, ntcrypto.NT_MODE_STRICT, tmp_pk.data_ptr(), hsig.data_ptr(), ids.data_ptr(),
-                          i_off.data_ptr(), i_len.data_ptr(), G, hbits.data_ptr())
-            be.dev_verify(0, sp, ntcrypto.NT_MODE_COFACTORLESS, vpk.data_ptr(), vsig.data_ptr(), cd2.data_ptr(),
-                          v_off.data_ptr(), v_len.data_ptr(), V, vbits.data_ptr())
-            be.dev_group_and(0, sp, first.data_ptr(), cnt.data_ptr(), G, vbits.data_ptr(), gbits.data_ptr())
+            be.dev_verify(0, sq, ntcrypto.NT_MODE_STRICT, tmp_pk.data_ptr(), hsig.data_ptr(), ids.data_ptr(),
+                          i_off.data_ptr(), i_len.data_ptr(), G, b["hbits"].data_ptr())
+            be.dev_verify(0, sq, ntcrypto.NT_MODE_COFACTORLESS, vpk.data_ptr(), vsig.data_ptr(), b["cd2"].data_ptr(),
+                          v_off.data_ptr(), v_len.data_ptr(), V, b["vbits"].data_ptr())
+            be.dev_group_and(0, sq, first.data_ptr(), cnt.data_ptr(), G, b["vbits"].data_ptr(), b["gbits"].data_ptr())
 
-    def verdicts(cached):
-        gb = np.unpackbits(gbits.cpu().numpy().view(np.uint8), bitorder="little")[:G].astype(bool)
+    def verdicts(cached, k):
+        b = bufs[k]
+        gb = np.unpackbits(b["gbits"].cpu().numpy().view(np.uint8), bitorder="little")[:G].astype(bool)
         if cached and keysort:   # un-permute the vote bits, AND per certificate on the host
-            vb = np.unpackbits(mbits.cpu().numpy().view(np.uint8), bitorder="little")[:V].astype(bool)
+            vb = np.unpackbits(b["mbits"].cpu().numpy().view(np.uint8), bitorder="little")[:V].astype(bool)
             orig = np.empty(V, bool)
             orig[perm] = vb
             gb = orig.reshape(G, quorum).all(axis=1)
         if cached and fused:   # header verdicts follow the V vote bits of the fused launch
-            hb = np.unpackbits(mbits.cpu().numpy().view(np.uint8), bitorder="little")[V:V + G].astype(bool)
+            hb = np.unpackbits(b["mbits"].cpu().numpy().view(np.uint8), bitorder="little")[V:V + G].astype(bool)
         else:
-            hb = np.unpackbits(hbits.cpu().numpy().view(np.uint8), bitorder="little")[:G].astype(bool)
-        idok = (hd2 == ids).all(dim=1).cpu().numpy()
+            hb = np.unpackbits(b["hbits"].cpu().numpy().view(np.uint8), bitorder="little")[:G].astype(bool)
+        idok = (b["hd2"] == ids).all(dim=1).cpu().numpy()
         return gb & hb & idok
 
     out = {}
     steps = max(1, min(args.steps, 5))
-    for cached in (True, False):
-        for _ in range(max(1, args.warmup)):
-            step(cached)
+    runs = [("keyset", True, nst)] + ([("keyset_one_stream", True, 1)] if nst > 1 and fused else []) + \
+        [("uncached", False, 1)]
+    for key, cached, ns in runs:
+        mode_streams[cached] = ns
+        kev.clear()
+        for i in range(max(1, args.warmup)):
+            step(cached, i)
         barrier()
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(stream)
-        for _ in range(steps):
-            step(cached, timed=True)
+        for st in streams[1:slots(cached)]:
+            st.wait_event(ev0)
+        for i in range(steps):
+            step(cached, i, timed=True)
+        for st in streams[1:slots(cached)]:
+            j = torch.cuda.Event()
+            j.record(st)
+            stream.wait_event(j)
         ev1.record(stream)
         barrier()
         wall = max_over_ranks(time.perf_counter() - t0)
         kms = ev0.elapsed_time(ev1) / steps
-        mism = int(max_over_ranks(int((verdicts(cached) != expect).sum())))
-        key = "keyset" if cached else "uncached"
+        bad = sum(int((verdicts(cached, k) != expect).sum()) for k in range(min(slots(cached), steps)))
+        mism = int(max_over_ranks(bad))
         out[key] = {"certs_per_s": round(G_total * steps / wall, 1),
                     "sig_verifies_per_s": round(G_total * (quorum + 1) * steps / wall, 1),
                     "ms_per_step": round(wall * 1e3 / steps, 3), "gpu_ms_per_step": round(kms, 3),
-                    "mismatches_vs_expected": mism}
-        if cached and fused and kev:
-            out[key]["roofline"] = keyset_roofline(np.mean([a.elapsed_time(b) for a, b in kev]), V + G)
+                    "streams": slots(cached), "mismatches_vs_expected": mism}
+        if key == "keyset" and fused and kev:
+            out[key]["roofline"] = keyset_roofline(np.mean([a.elapsed_time(b) for a, b in kev]), kms, V + G)
     ks.close()
     if world == 1 and not getattr(args, "no_cpu", False):
         out["cpu_baseline"] = cert_cpu_baseline(args, hdr, hlen, ids, tmp_pk, hsig, cpre, vpk, vsig, quorum, expect)
@@ -726,6 +788,9 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
             "workload": "cfg3: %d certificates, committee n=%d, %d votes + 1 header signature each, "
                         "%d-byte header preimage" % (G_total, nk, quorum, hlen),
             "scaling": "strong (certificates sharded over ranks)",
+            "pipelining": "keyset: consecutive steps (independent 100k-certificate batches) on two streams, each "
+                          "with its own digest / verdict buffers (the device API alternates its two key-cache "
+                          "stashes); keyset_one_stream: the same launches strictly back to back on one stream",
             "key_cache": {"comb_bits": ks_bits, "gb_per_device": round(ks_bytes / 1e9, 2),
                           "build_s": round(ks_build_s, 3),
                           "note": "per-key wide combs of -A (13 comb additions per [k]A at 20 bits; [s]B: 11 "
@@ -736,10 +801,16 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
             **out}
 
 
-def keyset_roofline(kernel_ms, nsig):
+def keyset_roofline(launch_ms, step_ms, nsig):
     """The config-3 key-cache launch (k_ed25519_verify_keyset, NT_MODE_MIXED) against
     the same v_mad_u64_u32 issue peak as the headline kernel; the instruction
-    count, issue share and HBM traffic come from the committed PMC profile."""
+    count, issue share and HBM traffic come from the committed PMC profile.
+    With steps alternating between two streams the launches of consecutive
+    batches overlap, so a launch's own start-to-end time (launch_ms, what rocprof
+    reports per dispatch) exceeds the GPU time per batch; the kernel's rate is
+    then taken over the smaller of the two (step_ms includes the step's digest
+    and group-AND launches, so it understates the kernel's rate slightly)."""
+    kernel_ms = min(launch_ms, step_ms)
     try:
         with open(os.path.join(ROOT, "profiles", "opcount.json")) as f:
             mads = float(json.load(f)["verify_cofactorless_keyset_mads"])
@@ -750,6 +821,7 @@ def keyset_roofline(kernel_ms, nsig):
     pkl = pk.get("per_launch", {})
     grid = pk.get("grid")
     return {"bound": "valu", "kernel": "k_ed25519_verify_keyset<mixed>", "kernel_ms": round(kernel_ms, 3),
+            "launch_ms": round(launch_ms, 3), "gpu_ms_per_step": round(step_ms, 3),
             "signatures_per_launch": nsig, "mads_per_signature": mads,
             "achieved": round(achieved, 3), "peak": round(MAD_PEAK_TS, 2), "unit": "Tmad/s",
             "frac": round(achieved / MAD_PEAK_TS, 4),

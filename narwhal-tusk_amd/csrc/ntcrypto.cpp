@@ -109,10 +109,11 @@ struct Device {
   // c+1 fill the CUs that chunk c's last waves leave idle.  Stream 2 has its own
   // verify workspace and key-cache stash.
   hipStream_t stream2 = nullptr;
-  hipEvent_t join2 = nullptr, ws2_done = nullptr;
+  hipEvent_t join2 = nullptr, ws2_done = nullptr, stash2_done = nullptr;
   DevBuf ws2, stash2, sort2;
   std::mutex mu;
   uint64_t dev_calls = 0;  // device-API verify calls (workspace alternation), under mu
+  uint64_t ks_calls = 0;   // device-API key-cache calls (stash alternation), under mu
   DevBuf d[B_NBUF];
   HostBuf h[B_NBUF];
   // Extra execution slots of the same device entry (NT_SLOTS, default 2 in
@@ -145,6 +146,7 @@ struct Device {
     if (sort2.p) (void)hipFree(sort2.p);
     if (join2) (void)hipEventDestroy(join2);
     if (ws2_done) (void)hipEventDestroy(ws2_done);
+    if (stash2_done) (void)hipEventDestroy(stash2_done);
     if (stream2 && stream2 != stream) (void)hipStreamDestroy(stream2);
     if (cstream && cstream != stream) (void)hipStreamDestroy(cstream);
     if (stream) (void)hipStreamDestroy(stream);
@@ -177,6 +179,7 @@ struct Device {
     for (auto& e : cev) NT_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     NT_TRY(hipEventCreateWithFlags(&join2, hipEventDisableTiming));
     NT_TRY(hipEventCreateWithFlags(&ws2_done, hipEventDisableTiming));
+    NT_TRY(hipEventCreateWithFlags(&stash2_done, hipEventDisableTiming));
     if (share) {
       d_combB = share->d_combB;
       owns_comb = false;
@@ -199,6 +202,8 @@ struct Device {
     if (hipMalloc(&d_ws, nt::ws_bytes_per_slot() * ws_slots) != hipSuccess) return NT_ENOMEM;
     NT_TRY(hipEventRecord(ws_done, stream));
     NT_TRY(hipEventRecord(stash_done, stream));
+    NT_TRY(hipEventRecord(ws2_done, stream));
+    NT_TRY(hipEventRecord(stash2_done, stream));
     NT_TRY(hipStreamSynchronize(stream));
     return NT_OK;
   }
@@ -259,17 +264,35 @@ struct Device {
     return NT_OK;
   }
 
-  // Key-cache launch on stream s with stash st: launches that use the shared
-  // d[B_STASH] (host chunks on `stream`, device-API calls on any stream) wait
-  // for its previous user and mark it, like d_ws; stash2 belongs to stream2.
-  // The key-grouping scratch (d[B_SORT] / sort2) goes with its stash.
+  // Key-cache launch on stream s with stash st: every launch waits for the
+  // previous user of its stash (d[B_STASH]: stash_done, stash2: stash2_done --
+  // host chunks on `stream` / stream2 and device-API calls on any stream) and
+  // marks it, like the [k]A workspaces.  The key-grouping scratch (d[B_SORT] /
+  // sort2) goes with its stash.
   template <class F>
   int keyset_launch(hipStream_t s, void* st, F&& launch) {
-    const bool shared = st == d[B_STASH].p;
-    if (shared && hipStreamWaitEvent(s, stash_done, 0) != hipSuccess) return NT_EHIP;
+    const hipEvent_t ev = st == d[B_STASH].p ? stash_done : (st == stash2.p ? stash2_done : nullptr);
+    if (ev && hipStreamWaitEvent(s, ev, 0) != hipSuccess) return NT_EHIP;
     if (launch() != hipSuccess) return NT_EHIP;
-    if (shared && hipEventRecord(stash_done, s) != hipSuccess) return NT_EHIP;
+    if (ev && hipEventRecord(ev, s) != hipSuccess) return NT_EHIP;
     return NT_OK;
+  }
+
+  // Grow a buffer that enqueue-only device-API calls may still be using: wait
+  // for its last user (the launch that recorded ev) before freeing it.
+  int grow_synced(DevBuf& b, size_t bytes, hipEvent_t ev) {
+    if (bytes <= b.cap) return NT_OK;
+    if (b.p && hipEventSynchronize(ev) != hipSuccess) return NT_EHIP;
+    return b.ensure(bytes);
+  }
+  // the stash / key-grouping scratch pair of slot k (0: d[B_STASH] / d[B_SORT],
+  // 1: stash2 / sort2) for launches of up to m signatures
+  int ensure_stash(int k, uint64_t m) {
+    DevBuf& st = k ? stash2 : d[B_STASH];
+    DevBuf& so = k ? sort2 : d[B_SORT];
+    const hipEvent_t ev = k ? stash2_done : stash_done;
+    const int rc = grow_synced(st, nt::keyset_stash_bytes(m), ev);
+    return rc != NT_OK ? rc : grow_synced(so, nt::keyset_sort_bytes(m), ev);
   }
 
   // ws2 holds >= blocks workspace slots; a grown buffer is freed only after its
@@ -1015,10 +1038,8 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
     if (ks) {
       uint64_t mc = 0;
       for (size_t c = 0; c < C; ++c) mc = std::max(mc, E[c + 1] - E[c]);
-      NT_CHK(dv.d[B_STASH].ensure(nt::keyset_stash_bytes(mc)));
-      NT_CHK(dv.d[B_SORT].ensure(nt::keyset_sort_bytes(mc)));
-      if (C > 1) NT_CHK(dv.stash2.ensure(nt::keyset_stash_bytes(mc)));
-      if (C > 1) NT_CHK(dv.sort2.ensure(nt::keyset_sort_bytes(mc)));
+      NT_CHK(dv.ensure_stash(0, mc));
+      if (C > 1) NT_CHK(dv.ensure_stash(1, mc));
       pd_meta = &ks->dev[dev_index(ctx, dv)];
     }
     uint8_t* hkey = dv.h[B_PK].as<uint8_t>();
@@ -1268,10 +1289,8 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
     NT_CHK(dv.h[B_OUT].ensure(words * 8));
     uint64_t mc = 0;
     for (const auto& c : ch) mc = std::max(mc, c.second - c.first);
-    NT_CHK(dv.d[B_STASH].ensure(nt::keyset_stash_bytes(mc)));
-    NT_CHK(dv.d[B_SORT].ensure(nt::keyset_sort_bytes(mc)));
-    if (ch.size() > 1) NT_CHK(dv.stash2.ensure(nt::keyset_stash_bytes(mc)));
-    if (ch.size() > 1) NT_CHK(dv.sort2.ensure(nt::keyset_sort_bytes(mc)));
+    NT_CHK(dv.ensure_stash(0, mc));
+    if (ch.size() > 1) NT_CHK(dv.ensure_stash(1, mc));
     for (size_t c = 0; c < ch.size(); ++c) {
       const uint64_t a = ch[c].first, b = ch[c].second;
       NT_CHK(msg_copy(dv, msg, off, len, lo, ms, c, a, b));
@@ -1364,13 +1383,15 @@ int nt_dev_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int dev, void
   NT_TRY(hipSetDevice(dv->ordinal));
   hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
   const auto& pd = ks->dev[dev];
-  // the device's stash, shared with the host entry points: ordered against
-  // every other user by stash_done, whatever the streams
+  // the device's two stashes, shared with the host entry points, each ordered
+  // against every other user by its event whatever the streams; successive
+  // device-API calls alternate between them (like nt_dev_ed25519_verify's
+  // workspaces), so batches on two streams can overlap
   std::lock_guard<std::mutex> lk(dv->mu);
-  NT_CHK(dv->d[B_STASH].ensure(nt::keyset_stash_bytes(n)));
-  NT_CHK(dv->d[B_SORT].ensure(nt::keyset_sort_bytes(n)));
-  void* stash = dv->d[B_STASH].p;
-  void* so = dv->d[B_SORT].p;
+  const int k = (int)(dv->ks_calls++ & 1u);
+  NT_CHK(dv->ensure_stash(k, n));
+  void* stash = k ? dv->stash2.p : dv->d[B_STASH].p;
+  void* so = k ? dv->sort2.p : dv->d[B_SORT].p;
   return dv->keyset_launch(s, stash, [&] {
     return nt::launch_verify_keyset(mode, ks->bits, d_key_idx, d_sig64, d_msg, d_off, d_len, n, pd.d_meta, pd.d_enc,
                                     pd.d_comb, ks->nkeys, dv->d_combB, stash, so, d_out_words, s);
