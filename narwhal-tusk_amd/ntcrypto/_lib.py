@@ -143,6 +143,22 @@ class Backend:
         """Small calls on host threads (include/ntcrypto.h)."""
         _check(self.lib.nt_set_small_call_path(self.ctx, int(mode), int(threads)), "nt_set_small_call_path")
 
+    def pinned(self, shape, dtype=np.uint8):
+        """A numpy array in nt_host_alloc memory (pinned, registered with every
+        device of the process): inputs placed there are DMA'd by the host entry
+        points without the staging copy.  Freed when the array is collected."""
+        dt = np.dtype(dtype)
+        count = int(np.prod(shape)) if np.ndim(shape) else int(shape)
+        nbytes = max(1, count * dt.itemsize)
+        p = self.lib.nt_host_alloc(nbytes)
+        if not p:
+            raise MemoryError("nt_host_alloc(%d)" % nbytes)
+        buf = (ctypes.c_uint8 * nbytes).from_address(p)
+        arr = np.frombuffer(buf, dtype=np.uint8, count=count * dt.itemsize).view(dt).reshape(shape)
+        import weakref
+        weakref.finalize(buf, self.lib.nt_host_free, ctypes.c_void_p(p))
+        return arr
+
     def call_counts(self):
         """(host-lane calls, GPU calls) of the host entry points so far."""
         h = np.zeros(1, np.uint64)
