@@ -244,12 +244,11 @@ def main():
     sig.copy_(torch.from_numpy(sig_h))
     msgs.copy_(torch.from_numpy(msg_h))
     words = (n + 63) // 64
-    # The headline: launches strictly back to back on one stream.  Reported
-    # beside it ("pipelined_two_streams"): consecutive steps (independent 1M
-    # batches) alternating between two streams, the way a verifier fed a stream
-    # of batches runs -- nt_dev_ed25519_verify alternates its two workspaces, so
-    # step i+1's waves may fill the SIMDs step i's last round leaves idle.
-    # NT_BENCH_STREAMS=2 makes that mode the headline (A/B).
+    # The headline: launches strictly back to back on one stream.
+    # NT_BENCH_STREAMS=2 (A/B only): consecutive steps alternate between two
+    # streams (nt_dev_ed25519_verify alternates its two workspaces, so the
+    # launches are independent) -- measured slower or equal for config 2
+    # (DESIGN.md §10), unlike config 3.
     nstreams = 2 if os.environ.get("NT_BENCH_STREAMS", "1") == "2" else 1
     streams = [stream, torch.cuda.Stream(dev)]
     outs = [torch.zeros(words, dtype=torch.int64, device=dev) for _ in range(2)]
@@ -339,36 +338,6 @@ def main():
             "parity": {"mismatches_vs_expected": mism, "checked": n * world},
             "input_gen_s": round(gen_s, 3)}
     line["streams"] = nstreams
-
-    # --------------- the same K batches with consecutive steps on alternating streams
-    if nstreams == 1:
-        barrier()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        e0.record(stream)
-        streams[1].wait_event(e0)
-        for i in range(args.steps):
-            st = streams[i % 2]
-            be.dev_verify(0, st.cuda_stream, ntcrypto.NT_MODE_STRICT, pk.data_ptr(), sig.data_ptr(),
-                          msgs.data_ptr(), off.data_ptr(), ln.data_ptr(), n, outs[i % 2].data_ptr())
-        j = torch.cuda.Event()
-        j.record(streams[1])
-        stream.wait_event(j)
-        e1.record(stream)
-        barrier()
-        pwall = max_over_ranks(time.perf_counter() - t0)
-        pm = 0
-        for o in outs[:min(2, args.steps)]:
-            g2 = np.unpackbits(o.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
-            pm += int((g2 != expect).sum())
-        line["pipelined_two_streams"] = {
-            "value": round(n * world * args.steps / pwall, 1), "ms_per_step": round(pwall * 1e3 / args.steps, 3),
-            "gpu_ms_per_step": round(e0.elapsed_time(e1) / args.steps, 3),
-            "mismatches_vs_expected": int(max_over_ranks(pm)),
-            "note": "not the headline: the same K 1M-verify steps with consecutive steps on two streams "
-                    "(nt_dev_ed25519_verify alternates its two workspaces), so a step's first waves may run "
-                    "in the previous step's last round"}
 
     # ------------------------------------------- same cfg2 batch through the host entry point
     # (caller buffers in ordinary host memory: PCIe-inclusive, never `value`)
