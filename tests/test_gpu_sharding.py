@@ -183,3 +183,50 @@ def test_chunked_host_calls_match(devices, monkeypatch):
             assert np.array_equal(a, b), (rnd, k)
     ks.close()
     be.close()
+
+
+def test_dev_api_batches_on_two_streams(pair):
+    """Device-API calls alternate between the device's two [k]A workspaces and
+    two key-cache stashes (include/ntcrypto.h): two different batches enqueued
+    alternately on two streams, many times over without a host sync, each into
+    its own output buffer, must keep their own verdicts (the corpus with and
+    without a bit flipped in every signature's s)."""
+    import torch
+    import ntcrypto
+    one, _ = pair
+    d = np.load(os.path.join(GOLD, "ed25519_corpus.npz"))
+    dev = torch.device("cuda", 0)
+    reps = 40                                    # 14,400 signatures per batch: one partial round
+    pk = torch.from_numpy(np.tile(d["pk"], (reps, 1))).to(dev)
+    sig_a = np.tile(d["sig"], (reps, 1))
+    sig_b = sig_a.copy()
+    sig_b[:, 40] ^= 1                            # s changes: every equation fails
+    sig = [torch.from_numpy(sig_a).to(dev), torch.from_numpy(sig_b).to(dev)]
+    msg = torch.from_numpy(np.ascontiguousarray(d["msg"])).to(dev)
+    off = torch.from_numpy(np.tile(d["off"], reps).astype(np.int64)).to(dev)
+    ln = torch.from_numpy(np.tile(d["len"], reps).astype(np.int64)).to(dev)
+    n = len(pk)
+    want = [np.tile(d["strict"], reps).astype(bool), None]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    outs = [torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev) for _ in range(2)]
+    uniq, inv = np.unique(d["pk"], axis=0, return_inverse=True)
+    ks = one.keyset(uniq)
+    kidx = torch.from_numpy(np.tile(inv.ravel().astype(np.uint32), reps).view(np.int32)).to(dev)
+    kouts = [torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev) for _ in range(2)]
+    torch.cuda.synchronize(dev)
+    for i in range(24):
+        k = i % 2
+        s = streams[k].cuda_stream
+        one.dev_verify(0, s, ntcrypto.NT_MODE_STRICT, pk.data_ptr(), sig[k].data_ptr(), msg.data_ptr(),
+                       off.data_ptr(), ln.data_ptr(), n, outs[k].data_ptr())
+        ks.dev_verify(0, s, ntcrypto.NT_MODE_STRICT, kidx.data_ptr(), sig[k].data_ptr(), msg.data_ptr(),
+                      off.data_ptr(), ln.data_ptr(), n, kouts[k].data_ptr())
+    torch.cuda.synchronize(dev)
+    for k in range(2):
+        for o in (outs[k], kouts[k]):
+            got = np.unpackbits(o.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+            if k == 0:
+                assert np.array_equal(got, want[0])
+            else:
+                assert not got.any()
+    ks.close()
