@@ -140,3 +140,42 @@ def test_cfg4_sha512_full_size(env):
     assert changed.tolist() == [j]
     b = data[j * ml:(j + 1) * ml].cpu().numpy().tobytes()
     assert d1[j].tobytes() == hashlib.sha512(b).digest()[:32]
+
+
+def test_random_corruptions_vs_oracle_200k(env, oracle):
+    """200k GPU-signed verifications with a seeded mix of corruptions (bit flips
+    in R, s, A and the message; s + L; s with bit 255; R replaced by a random
+    encoding; A replaced by another key) and 32-1,024-B messages, each verdict
+    equal to the CPU oracle's: the half-size lattice reduction (Lehmer batches),
+    the joint ladder and the 24-bit comb of B meet ~200k different scalars."""
+    torch, be, dev, sp = env.torch, env.be, env.dev, env.sp
+    rng = np.random.default_rng(2024)
+    n = 200_000
+    lens = rng.integers(32, 1025, n).astype(np.uint64)
+    off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    msg = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    pk, sig = be.sign_batch(seeds, msg, off, lens)
+    pk, sig, msg = pk.copy(), sig.copy(), msg.copy()
+    kind = rng.integers(0, 10, n)                         # 0-2: untouched
+    L = 2 ** 252 + 27742317777372353535851937790883648493
+    for i in np.nonzero(kind == 3)[0]:
+        sig[i, rng.integers(0, 32)] ^= np.uint8(1 << rng.integers(0, 8))        # R
+    for i in np.nonzero(kind == 4)[0]:
+        sig[i, 32 + rng.integers(0, 32)] ^= np.uint8(1 << rng.integers(0, 8))   # s
+    for i in np.nonzero(kind == 5)[0]:
+        pk[i, rng.integers(0, 32)] ^= np.uint8(1 << rng.integers(0, 8))         # A
+    for i in np.nonzero(kind == 6)[0]:
+        msg[int(off[i]) + int(rng.integers(0, int(lens[i])))] ^= 1            # message
+    for i in np.nonzero(kind == 7)[0]:                                          # s + L (< 2^256)
+        s = int.from_bytes(sig[i, 32:].tobytes(), "little") + L
+        sig[i, 32:] = np.frombuffer(s.to_bytes(32, "little"), np.uint8)
+    sig[kind == 8, 63] |= 0x80                                                  # s bit 255
+    r9 = np.nonzero(kind == 9)[0]
+    sig[r9[: len(r9) // 2], :32] = rng.integers(0, 256, (len(r9) // 2, 32), dtype=np.uint8)  # random R
+    pk[r9[len(r9) // 2:]] = pk[(r9[len(r9) // 2:] + 1) % n]                    # another key
+    got = be.verify_strict(pk, sig, msg, off, lens)
+    want = oracle.verify_strict_many(pk, sig, msg, off, lens, nthreads=16).astype(bool)
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, [(int(i), int(kind[i])) for i in bad[:20]]
+    assert want[kind <= 2].all() and not want[(kind >= 4) & (kind <= 8)].any()
