@@ -352,3 +352,43 @@ def test_keyset_key_grouped_order(be, corpus, monkeypatch):
     gb = ks.verify_batch_groups(kidx, np.tile(g["sig"], (reps, 1)), first, cnt, np.tile(g["msg32"], (reps, 1)))
     assert np.array_equal(gb, np.tile(g["expect"], reps).astype(bool))
     ks.close()
+
+
+def test_verify_ragged_message_lengths(be, oracle):
+    """One verify launch whose lanes hash very different message lengths (the
+    k = SHA-512(R || A || M) loop runs per lane: 0 B up to 300 kB, padding
+    boundaries 111/112/239/240 B around the 64-byte R || A prefix), honest and
+    corrupted, against the oracle -- in strict and cofactorless mode."""
+    import ntcrypto
+    rng = np.random.default_rng(17)
+    choices = np.array([0, 1, 47, 48, 63, 64, 111, 112, 127, 128, 175, 176, 239, 240, 1000, 65536, 300000])
+    n = 2048
+    lens = choices[rng.integers(0, len(choices), n)].astype(np.uint64)
+    lens[rng.integers(0, n, 3)] = 300000
+    off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    data = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    pk, sig = be.sign_batch(seeds, data, off, lens)
+    sig = sig.copy()
+    flip = rng.random(n) < 0.3
+    sig[flip, 32] ^= 1
+    got = be.verify_strict(pk, sig, data, off, lens)
+    want = oracle.verify_strict_many(pk, sig, data, off, lens, nthreads=8).astype(bool)
+    assert np.array_equal(got, want)
+    assert np.array_equal(got, ~flip)
+    # cofactorless (verify_batch's per-entry rule) on the device entry point,
+    # which takes arbitrary messages; a sample checked one by one on the oracle
+    import torch
+    dev = torch.device("cuda", 0)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
+         (("pk", pk), ("sig", sig), ("data", data), ("off", off.view(np.int64)), ("len", lens.view(np.int64)))}
+    out = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    st = torch.cuda.Stream(dev)
+    be.dev_verify(0, st.cuda_stream, ntcrypto.NT_MODE_COFACTORLESS, t["pk"].data_ptr(), t["sig"].data_ptr(),
+                  t["data"].data_ptr(), t["off"].data_ptr(), t["len"].data_ptr(), n, out.data_ptr())
+    torch.cuda.synchronize(dev)
+    cof = np.unpackbits(out.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+    assert np.array_equal(cof, ~flip)
+    for i in rng.choice(n, 64, replace=False):
+        m = data[int(off[i]):int(off[i] + lens[i])].tobytes()
+        assert cof[i] == oracle.verify_cofactorless(pk[i].tobytes(), sig[i].tobytes(), m), int(i)
