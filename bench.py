@@ -452,6 +452,26 @@ def bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_r
            "valu_issue_share": round(pv["valu_issue_share_4cyc"], 3) if "valu_issue_share_4cyc" in pv else None,
            "note": "k_sha512_pipe: per 64 messages a producer wave expands K+W into LDS, a consumer wave runs the rounds; bound by the consumer wave's serial per-block stream (latency-bound, SURVEY H2), not HBM; valu_issue_share from the PMC profile (256 consumer + 256 producer waves on 1,024 SIMDs)",
            "spot_check_ok": bool(ok)}
+    # the same shard through the host entry point from pinned host memory
+    # (PCIe-inclusive: BASELINE.md reports GPU numbers with and without H2D)
+    if m:
+        host = be.pinned((m * ml,))
+        host[...] = data[:m * ml].cpu().numpy()
+        hoff = np.arange(m, dtype=np.uint64) * ml
+        hlen = np.full(m, ml, np.uint64)
+        hd = be.sha512_trunc32(host, hoff, hlen)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(2):
+            hd = be.sha512_trunc32(host, hoff, hlen)
+        barrier()
+        hwall = max_over_ranks((time.perf_counter() - t0) / 2)
+        res["host_api"] = {"gb_per_s": round(m_total * ml / hwall / 1e9, 2), "ms_per_call": round(hwall * 1e3, 3),
+                           "digests_equal_device_path": bool(np.array_equal(hd, out.cpu().numpy())),
+                           "note": "nt_sha512_trunc32 on the shard from nt_host_alloc (pinned) memory: %.2f GB "
+                                   "over PCIe per call, copies of chunk c+1 under the kernel of chunk c"
+                                   % (m * ml / 1e9)}
+        del host
     if world == 1 and not args.no_cpu:
         res["cpu_baseline"] = sha_cpu_baseline(args, data, out, m, ml)
     return res
