@@ -86,10 +86,14 @@ NT_HD NT_INLINE int32_t wcomb_digit(uint32_t d[8], uint32_t& carry) {
   return (int32_t)raw - (int32_t)(carry << W);
 }
 
-// acc += [x]P with P's wide comb.  The table load of digit i+1 is issued right
-// after the multiplies that consume entry i, so its latency (a random 128-B
-// line) overlaps the rest of the addition.
-template <class WComb>
+// acc += [x]P with P's wide comb (kFromIdentity: acc = [x]P, the first entry
+// taken as the starting point instead of added to the identity).  The table
+// load of digit i+1 is issued right after the multiplies that consume entry i,
+// so its latency (a random 128-B line) overlaps the rest of the addition.
+#ifndef NT_COMB_FROM_ID
+#define NT_COMB_FROM_ID 1
+#endif
+template <class WComb, bool kFromIdentity = false>
 NT_HD NT_INLINE void wcomb_acc(ge_p3& acc, const uint32_t x[8], const WComb& wc) {
   constexpr int W = WComb::kBits, P = CombGeom<W>::kPos;
   uint32_t d[8], carry = 0;
@@ -98,8 +102,18 @@ NT_HD NT_INLINE void wcomb_acc(ge_p3& acc, const uint32_t x[8], const WComb& wc)
   int32_t dg = wcomb_digit<W>(d, carry);
   ge_niels ne;
   wc.load(0, (uint32_t)(dg < 0 ? -dg : dg), ne);
+  int pos0 = 0;
+  if (kFromIdentity && NT_COMB_FROM_ID) {
+    ge_niels_cneg(ne, dg < 0);
+    ge_p3_from_niels(acc, ne);
+    dg = wcomb_digit<W>(d, carry);
+    wc.load(1, (uint32_t)(dg < 0 ? -dg : dg), ne);
+    pos0 = 1;
+  } else if (kFromIdentity) {
+    ge_p3_0(acc);  // -DNT_COMB_FROM_ID=0 (A/B builds): add the first entry to the identity
+  }
 #pragma unroll 1
-  for (int pos = 0; pos < P; ++pos) {
+  for (int pos = pos0; pos < P; ++pos) {
     ge_niels_cneg(ne, dg < 0);
     fe PP, MM, TT;
     ge_add_niels_1(PP, MM, TT, acc, ne);
@@ -444,8 +458,7 @@ NT_HD NT_INLINE uint32_t cached_point(ge_p3& acc, uint32_t meta, const uint32_t 
   if (is_strict<MODE>(meta)) okj &= (meta & kKeySmallOrder) ? 0u : 1u;
   uint32_t k[8];
   hram_scalar(k, Rw, Aw, msg, len);
-  ge_p3_0(acc);
-  wcomb_acc(acc, k, ca);
+  wcomb_acc<WCombA, true>(acc, k, ca);
   wcomb_acc(acc, Sw, cb);
   return okj;
 }
@@ -532,8 +545,7 @@ NT_HD NT_INLINE void sign_one(uint32_t Aw[8], uint32_t Rw[8], uint32_t s[8], con
   sc_reduce256(ared, a);
   ge_p3 P;
   ge_p2 P2;
-  ge_p3_0(P);
-  wcomb_acc(P, ared, wb);
+  wcomb_acc<WComb, true>(P, ared, wb);
   ge_p3_to_p2(P2, P);
   ge_tobytes_w(Aw, P2);
 
@@ -541,8 +553,7 @@ NT_HD NT_INLINE void sign_one(uint32_t Aw[8], uint32_t Rw[8], uint32_t s[8], con
   uint32_t hr[16], r[8];
   sha512_out_words(hr, st, 16);
   sc_reduce512(r, hr);
-  ge_p3_0(P);
-  wcomb_acc(P, r, wb);
+  wcomb_acc<WComb, true>(P, r, wb);
   ge_p3_to_p2(P2, P);
   ge_tobytes_w(Rw, P2);
 

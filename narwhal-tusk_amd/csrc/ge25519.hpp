@@ -113,6 +113,21 @@ NT_HD NT_INLINE void ge_add_niels(ge_cp& r, const ge_p3& p, const ge_niels& q) {
   ge_add_niels_2(r, PP, MM, TT, p.Z);
 }
 
+// The first point of a comb sum that starts at the identity: an affine niels
+// entry (y+x, y-x, 2dxy) taken as (2x : 2y : 2 : 2xy), T = (2dxy) / d -- one
+// multiply instead of an addition to the identity (7).
+NT_HD NT_INLINE void ge_p3_from_niels(ge_p3& r, const ge_niels& q) {
+  fe dinv;
+  fe_const(dinv, kFeDInv);
+  fe_sub(r.X, q.ypx, q.ymx);
+  fe_carry(r.X);
+  fe_add(r.Y, q.ypx, q.ymx);
+  fe_carry(r.Y);
+  fe_0(r.Z);
+  r.Z.v[0] = 2;
+  fe_mul(r.T, q.xy2d, dinv);  // xy2d: niels (< 2^26) or its fe_neg (f side)
+}
+
 // Affine niels entry of the projective point (X:Y:Z), given zi = Z^-1.
 NT_HD NT_INLINE void ge_niels_from(ge_niels& q, const fe& X, const fe& Y, const fe& zi) {
   fe x, y, d2;

@@ -1,4 +1,5 @@
-"""Probe of the phased verify kernel on the GPU: one launch at a time with
+"""Probe of a verify launch on the GPU (written for the phased-kernel experiment,
+DESIGN.md §10, which is not in the product): one launch at a time with
 timestamps, so a slow or stuck step names itself (faulthandler dumps the
 Python stack if a step takes longer than the watchdog)."""
 import faulthandler
