@@ -586,14 +586,14 @@ uint32_t wcomb_fill_batch(int bits) { return (uint32_t)comb_size(bits, 3); }
 int bcomb_bits() { return kBCombBits; }
 // verify grid: one 512-signature block per workspace slot, at most ws_slots
 uint64_t verify_grid(uint64_t n, uint32_t ws_slots) {
-  const uint64_t blocks = (n + 2 * kBlock - 1) / (2 * kBlock);  // two signatures per lane
+  const uint64_t blocks = (n + kVPer * kBlock - 1) / (kVPer * kBlock);  // kVPer signatures per lane
   return blocks < ws_slots ? blocks : ws_slots;
 }
 
 // signatures one wave of resident workgroups covers (every CU full at the
 // kernel's occupancy): launches sized in whole rounds leave no partial last wave
 uint64_t keyset_round_sigs(uint32_t cus) { return (uint64_t)cus * 4 * keyset_occ() * 64 * keyset_per_lane(); }
-uint64_t verify_round_sigs(uint32_t cus) { return (uint64_t)cus * verify_occupancy() * 2 * kBlock; }
+uint64_t verify_round_sigs(uint32_t cus) { return (uint64_t)cus * verify_occupancy() * kVPer * kBlock; }
 // signatures per lane of a key-cache launch (one inversion each): 8 (the
 // 4 / 6 / 8 / 12 / 16 A/B in DESIGN.md §5.2); NT_KEYSET_PER_LANE in
 // [1, kKsPerLane] overrides it for A/B runs

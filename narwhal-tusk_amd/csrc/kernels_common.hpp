@@ -12,6 +12,11 @@
 namespace nt {
 
 constexpr int kBlock = 256;
+#ifndef NT_VERIFY_PER_LANE
+#define NT_VERIFY_PER_LANE 2
+#endif
+// signatures per lane per block iteration of k_ed25519_verify (1 or 2; A/B builds)
+constexpr int kVPer = NT_VERIFY_PER_LANE;
 constexpr int kAEntries = 18;         // j*(+-A) and j*(-R), |digit| in 0..8
 constexpr int kAQuads = 10;           // uint4 per cached entry (40 words)
 
