@@ -452,6 +452,27 @@ def bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_r
            "valu_issue_share": round(pv["valu_issue_share_4cyc"], 3) if "valu_issue_share_4cyc" in pv else None,
            "note": "k_sha512_pipe: per 64 messages a producer wave expands K+W into LDS, a consumer wave runs the rounds; bound by the consumer wave's serial per-block stream (latency-bound, SURVEY H2), not HBM; valu_issue_share from the PMC profile (256 consumer + 256 producer waves on 1,024 SIMDs)",
            "spot_check_ok": bool(ok)}
+    # the shard one GPU holds when the driver runs config 4 on 8 GPUs
+    # (16,384 / 8 = 2,048 messages = 32 consumer waves): its per-GPU rate
+    m8 = (m_total + 7) // 8
+    if world == 1 and m >= m8 > 0:
+        def step8():
+            be.dev_sha512(0, sp, data.data_ptr(), off.data_ptr(), ln.data_ptr(), m8, out.data_ptr())
+        step8()
+        barrier()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(steps):
+            step8()
+        e1.record(stream)
+        barrier()
+        k8 = e0.elapsed_time(e1) / steps
+        res["shard_of_8"] = {"messages": m8, "kernel_ms": round(k8, 3),
+                             "gb_per_s_per_gpu": round(m8 * ml / (k8 * 1e-3) / 1e9, 2),
+                             "note": "one GPU's share of config 4 at 8 GPUs: the same serial per-message chain "
+                                     "(~3,907 blocks), 8x fewer messages, so the per-GPU rate is 1/8 and the "
+                                     "8-GPU aggregate stays at the 1-GPU figure"}
     # the same shard through the host entry point from pinned host memory
     # (PCIe-inclusive: BASELINE.md reports GPU numbers with and without H2D)
     if m:
