@@ -9,7 +9,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "narwhal-tusk_amd"))
 faulthandler.dump_traceback_later(int(os.environ.get("PROBE_WATCHDOG", "60")), repeat=True)
 T0 = time.time()
