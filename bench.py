@@ -809,6 +809,13 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                     "streams": slots(cached), "mismatches_vs_expected": mism}
         if key == "keyset" and fused and kev:
             out[key]["roofline"] = keyset_roofline(np.mean([a.elapsed_time(b) for a, b in kev]), kms, V + G)
+    if world == 1 and fused and os.environ.get("NT_BENCH_SHARDS", "1") != "0":
+        out["shard_of"] = bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, stream, barrier, G, quorum,
+                                            dict(hdr_flat=hdr_flat, h_off=h_off, h_len=h_len, cpre=cpre, c_off=c_off,
+                                                 c_len=c_len, ids=ids, vkey=vkey, hkey=hkey, vsig=vsig, hsig=hsig,
+                                                 v_off=v_off, v_len=v_len, i_off=i_off, i_len=i_len, first=first,
+                                                 cnt=cnt),
+                                            expect, out["keyset"]["certs_per_s"])
     ks.close()
     if world == 1 and not getattr(args, "no_cpu", False):
         out["cpu_baseline"] = cert_cpu_baseline(args, hdr, hlen, ids, tmp_pk, hsig, cpre, vpk, vsig, quorum, expect)
@@ -827,6 +834,89 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                           "launches": "per step: 2 SHA-512 (header ids, certificate digests), 1 NT_MODE_MIXED key-cache "
                                       "verify (67 votes cofactorless + the header signature strict), 1 group AND"},
             **out}
+
+
+def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, stream, barrier, G, quorum, t, expect, rate1):
+    """Config 3's 2/4/8-GPU shards rehearsed on this GPU (BASELINE configs[2] is
+    strong-scaled: each of N GPUs verifies G/N certificates): the first G/N
+    certificates through the same fused step (2 digests, one NT_MODE_MIXED
+    key-cache launch, group AND; consecutive steps on two streams with their
+    own buffers), timed the same way.  `per_gpu_vs_1gpu` = this shard's
+    certificates/s on one GPU / the full batch's: what each GPU of an N-GPU run
+    keeps of the 1-GPU rate (the key-cache launch plan, ks_plan.hpp, sizes the
+    persistent grid and chunks to the shard)."""
+    res = {}
+    steps = max(1, min(args.steps, 5))
+    nst = len(streams)
+    for N in (2, 4, 8):
+        Gs = G // N
+        Vs = Gs * quorum
+        mkey = torch.cat([t["vkey"][:Vs], t["hkey"][:Gs] + torch.iinfo(torch.int32).min]).contiguous()
+        msig = torch.cat([t["vsig"][:Vs], t["hsig"][:Gs]]).contiguous()
+        m_off = torch.cat([t["v_off"][:Vs], Gs * 32 + t["i_off"][:Gs]]).contiguous()
+        m_len = torch.cat([t["v_len"][:Vs], t["i_len"][:Gs]]).contiguous()
+        bufs = []
+        for _ in range(nst):
+            b = {"hd2": torch.empty((Gs, 32), dtype=torch.uint8, device=dev),
+                 "msgbuf": torch.empty((2 * Gs, 32), dtype=torch.uint8, device=dev),
+                 "gbits": torch.zeros(((Gs + 63) // 64,), dtype=torch.int64, device=dev),
+                 "mbits": torch.zeros(((Vs + Gs + 63) // 64 + 1,), dtype=torch.int64, device=dev)}
+            b["msgbuf"][Gs:] = t["ids"][:Gs]
+            bufs.append(b)
+        kev = []
+
+        def step(i, timed=False):
+            st = streams[i % nst]
+            sq = st.cuda_stream
+            b = bufs[i % nst]
+            be.dev_sha512(0, sq, t["hdr_flat"].data_ptr(), t["h_off"].data_ptr(), t["h_len"].data_ptr(), Gs,
+                          b["hd2"].data_ptr())
+            be.dev_sha512(0, sq, t["cpre"].data_ptr(), t["c_off"].data_ptr(), t["c_len"].data_ptr(), Gs,
+                          b["msgbuf"].data_ptr())
+            if timed:
+                kev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                kev[-1][0].record(st)
+            ks.dev_verify(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(),
+                          m_off.data_ptr(), m_len.data_ptr(), Vs + Gs, b["mbits"].data_ptr())
+            if timed:
+                kev[-1][1].record(st)
+            be.dev_group_and(0, sq, t["first"].data_ptr(), t["cnt"].data_ptr(), Gs, b["mbits"].data_ptr(),
+                             b["gbits"].data_ptr())
+
+        for i in range(max(1, args.warmup)):
+            step(i)
+        barrier()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for st in streams[1:]:
+            st.wait_event(ev0)
+        for i in range(steps):
+            step(i, timed=True)
+        for st in streams[1:]:
+            j = torch.cuda.Event()
+            j.record(st)
+            stream.wait_event(j)
+        ev1.record(stream)
+        barrier()
+        wall = time.perf_counter() - t0
+        bad = 0
+        for k in range(min(nst, steps)):
+            b = bufs[k]
+            gb = np.unpackbits(b["gbits"].cpu().numpy().view(np.uint8), bitorder="little")[:Gs].astype(bool)
+            hb = np.unpackbits(b["mbits"].cpu().numpy().view(np.uint8), bitorder="little")[Vs:Vs + Gs].astype(bool)
+            idok = (b["hd2"] == t["ids"][:Gs]).all(dim=1).cpu().numpy()
+            bad += int(((gb & hb & idok) != expect[:Gs]).sum())
+        rate = Gs * steps / wall
+        res[str(N)] = {"certificates": Gs, "signatures_per_launch": Vs + Gs, "certs_per_s": round(rate, 1),
+                       "ms_per_step": round(wall * 1e3 / steps, 3),
+                       "gpu_ms_per_step": round(ev0.elapsed_time(ev1) / steps, 3),
+                       "keyset_launch_ms": round(float(np.mean([a.elapsed_time(b) for a, b in kev])), 3),
+                       "per_gpu_vs_1gpu": round(rate / rate1, 3), "mismatches_vs_expected": bad}
+    res["note"] = ("one GPU running the first G/N certificates of the same batch, as rank r of an N-GPU run would "
+                   "(nd.shard); per_gpu_vs_1gpu >= 0.9 means the N-GPU aggregate stays within 10% of linear")
+    return res
 
 
 def keyset_roofline(launch_ms, step_ms, nsig):

@@ -3,8 +3,8 @@
 #include "k_keyset.inc"
 
 namespace nt {
-template hipError_t launch_keyset_m<kCofactorless, 20>(uint64_t, const uint32_t*, const uint8_t*, const uint8_t*,
+template hipError_t launch_keyset_m<kCofactorless, 20>(const KsPlan&, const uint32_t*, const uint8_t*, const uint8_t*,
                                              const uint64_t*, const uint64_t*, uint64_t, const uint32_t*,
                                              const uint32_t*, const uint32_t*, uint32_t, const uint32_t*,
-                                             void*, uint64_t*, const uint32_t*, uint8_t*, uint32_t, hipStream_t);
+                                             void*, uint64_t*, const uint32_t*, uint8_t*, uint32_t*, hipStream_t);
 }  // namespace nt

@@ -496,31 +496,40 @@ static bool keyset_sort_enabled() {
   return on;
 }
 
+// d_sort layout: [16 words: chunk counter][hist 4096][cursor 4096][perm m][verdict bytes m]
+constexpr size_t kSortHdr = 64;
 size_t keyset_sort_bytes(uint64_t n) {
   const uint64_t m = n < kKsMaxPerLaunch ? n : kKsMaxPerLaunch;
-  return 2 * kSortBuckets * 4 + (size_t)m * 5 + 64;
+  return kSortHdr + 2 * kSortBuckets * 4 + (size_t)m * 5 + 64;
+}
+
+KsPlan keyset_plan(uint64_t n, uint32_t cus) {
+  static const int force = env_occ("NT_KEYSET_WAVES", 0, 2, 3);
+  return ks_plan(n, cus, keyset_per_lane(), force);
 }
 
 hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                                 const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                                 const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
                                 const uint32_t* d_combB, void* d_stash, void* d_sort, uint64_t* d_out_words,
-                                hipStream_t s) {
+                                uint32_t cus, hipStream_t s) {
+  if (!d_sort || !d_stash) return hipErrorInvalidValue;
+  uint32_t* ctr = (uint32_t*)d_sort;
+  uint32_t* hist = ctr + kSortHdr / 4;
+  uint32_t* cursor = hist + kSortBuckets;
+  uint32_t* p = cursor + kSortBuckets;
   // launches of at most kKsMaxPerLaunch signatures reuse one stash (stream-ordered)
   for (uint64_t lo = 0; lo < n; lo += kKsMaxPerLaunch) {
     const uint64_t m = n - lo < kKsMaxPerLaunch ? n - lo : kKsMaxPerLaunch;
-    const uint32_t per_lane = keyset_per_lane();
-    const uint64_t blocks = keyset_blocks(m, per_lane);
+    const KsPlan pl = keyset_plan(m, cus);
     const uint32_t* perm = nullptr;
     uint8_t* bytes = nullptr;
-    if (d_sort && keyset_sort_enabled() && m >= kSortMin && nkeys + 1 <= kSortBuckets) {
-      uint32_t* hist = (uint32_t*)d_sort;
-      uint32_t* cursor = hist + kSortBuckets;
-      uint32_t* p = cursor + kSortBuckets;
+    hipError_t e = hipMemsetAsync(ctr, 0, 4, s);
+    if (e != hipSuccess) return e;
+    if (keyset_sort_enabled() && m >= kSortMin && nkeys + 1 <= kSortBuckets) {
       bytes = (uint8_t*)(p + m);
       const int mixed = mode == kMixed;
-      hipError_t e = hipMemsetAsync(hist, 0, 4ull * (nkeys + 1), s);
-      if (e != hipSuccess) return e;
+      if ((e = hipMemsetAsync(hist, 0, 4ull * (nkeys + 1), s)) != hipSuccess) return e;
       const uint32_t hb = (uint32_t)((m + kBlock - 1) / kBlock < 2048 ? (m + kBlock - 1) / kBlock : 2048);
       hipLaunchKernelGGL(k_key_hist, dim3(hb), dim3(kBlock), 0, s, d_key_idx + lo, m, mixed, nkeys, hist);
       hipLaunchKernelGGL(k_key_scan, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)hist, nkeys + 1, cursor);
@@ -531,9 +540,8 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
       perm = p;
     }
 #define NT_KS_ARGS                                                                                           \
-  blocks, d_key_idx + lo, d_sig + 64 * lo, d_msg, d_off + lo, d_len + lo, m, d_meta, d_enc, d_combA, nkeys, \
-      d_combB, d_stash, d_out_words + lo / 64, perm, bytes, per_lane, s
-    hipError_t e;
+  pl, d_key_idx + lo, d_sig + 64 * lo, d_msg, d_off + lo, d_len + lo, m, d_meta, d_enc, d_combA, nkeys,     \
+      d_combB, d_stash, d_out_words + lo / 64, perm, bytes, ctr, s
     if (key_bits == kKeyCombWide)
       e = mode == kStrict   ? launch_keyset_m<kStrict, kKeyCombWide>(NT_KS_ARGS)
           : mode == kMixed  ? launch_keyset_m<kMixed, kKeyCombWide>(NT_KS_ARGS)
@@ -594,21 +602,18 @@ uint64_t verify_grid(uint64_t n, uint32_t ws_slots) {
 // kernel's occupancy): launches sized in whole rounds leave no partial last wave
 uint64_t keyset_round_sigs(uint32_t cus) { return (uint64_t)cus * 4 * keyset_occ() * 64 * keyset_per_lane(); }
 uint64_t verify_round_sigs(uint32_t cus) { return (uint64_t)cus * verify_occupancy() * kVPer * kBlock; }
-// signatures per lane of a key-cache launch (one inversion each): 8 (the
-// 4 / 6 / 8 / 12 / 16 A/B in DESIGN.md §5.2); NT_KEYSET_PER_LANE in
-// [1, kKsPerLane] overrides it for A/B runs
+// most rows (signatures per lane) of a key-cache chunk, one inversion each: 8
+// (the 4 / 6 / 8 / 12 / 16 A/B in DESIGN.md §5.2); NT_KEYSET_PER_LANE in
+// [1, kKsPerLane] caps it for A/B runs
 uint32_t keyset_per_lane() {
   static const uint32_t m = (uint32_t)env_occ("NT_KEYSET_PER_LANE", kKsPerLane, 1, kKsPerLane);
   return m;
 }
-uint64_t keyset_blocks(uint64_t n, uint32_t per_lane) {
-  return (n + (uint64_t)per_lane * kBlock - 1) / ((uint64_t)per_lane * kBlock);
-}
-// stash of one launch (<= kKsMaxPerLaunch signatures: 1.25 GiB at most):
-// blocks * per_lane * kBlock <= n + per_lane * kBlock slots of kKsQuads quads
-size_t keyset_stash_bytes(uint64_t n) {
+// stash of one launch (<= kKsMaxPerLaunch signatures): waves x (most rows of a
+// chunk) x 64 lanes x 160 B, and waves x pmax <= rows + waves <= n / 64 + 1 + 12 cus
+size_t keyset_stash_bytes(uint64_t n, uint32_t cus) {
   const uint64_t m = n < kKsMaxPerLaunch ? n : kKsMaxPerLaunch;
-  return (size_t)(m + (uint64_t)kKsPerLane * kBlock) * kKsQuads * 16;
+  return (size_t)(m + 64 + (uint64_t)64 * 12 * cus) * kKsQuads * 16;
 }
 size_t ws_bytes_per_slot() { return (size_t)kAEntries * kAQuads * kBlock * 16; }
 

@@ -4,6 +4,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "ks_plan.hpp"
 #include "nt_common.hpp"
 
 namespace nt {
@@ -30,17 +31,19 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
                                 const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                                 const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
                                 const uint32_t* d_combB, void* d_stash, void* d_sort, uint64_t* d_out_words,
-                                hipStream_t s);
-// scratch of launch_verify_keyset's key-grouped order (d_sort; may be null = input order)
+                                uint32_t cus, hipStream_t s);
+// scratch of launch_verify_keyset: the chunk counter and the key-grouped order (d_sort, required)
 size_t keyset_sort_bytes(uint64_t n);
-// key-cache verification: blocks of a launch over n signatures and the per-lane
-// stash it needs (d_stash above)
+// the plan of one key-cache launch over n signatures on a device of `cus` CUs (ks_plan.hpp;
+// NT_KEYSET_WAVES = 2 / 3 forces the waves per SIMD, NT_KEYSET_PER_LANE caps the rows per chunk)
+KsPlan keyset_plan(uint64_t n, uint32_t cus);
+// signatures one full round of the launch covers (host-side chunk sizing)
 uint64_t keyset_round_sigs(uint32_t cus);
 uint64_t verify_grid(uint64_t n, uint32_t ws_slots);  // blocks of a launch_verify
 uint64_t verify_round_sigs(uint32_t cus);
 uint32_t keyset_per_lane();
-uint64_t keyset_blocks(uint64_t n, uint32_t per_lane);
-size_t keyset_stash_bytes(uint64_t n);
+// per-wave stash of a launch over n signatures (d_stash above)
+size_t keyset_stash_bytes(uint64_t n, uint32_t cus);
 size_t wcomb_bytes_per_key(int bits);
 size_t wcomb_bases_bytes_per_key(int bits);
 size_t wcomb_fill_tmp_bytes_per_key(int bits);

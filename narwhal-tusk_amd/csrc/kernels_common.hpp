@@ -110,12 +110,14 @@ struct WsATab {
 constexpr int kKsPerLane = NT_KS_PER_LANE;
 constexpr int kKsQuads = 10;  // X, Y, Z, prefix: 40 words per (signature, lane)
 
-// Per-lane stash in global memory, layout [block][j][quad][lane] of uint4
-// (lane-minor: a wave's 16-byte accesses are contiguous); a block's region is
-// per_lane * kKsQuads * kBlock quads.
+// Per-lane stash in global memory, layout [wave][j][quad][lane] of uint4
+// (lane-minor: a wave's 16-byte accesses are contiguous); a wave's region is
+// (most rows of a chunk) * kKsQuads * 64 quads.
 struct KsStash {
-  uint4* base;  // this block's region
-  NT_D NT_INLINE uint4* at(int j, int q) const { return base + ((size_t)(j * kKsQuads + q) * kBlock + threadIdx.x); }
+  uint4* base;  // this wave's region
+  NT_D NT_INLINE uint4* at(int j, int q) const {
+    return base + ((size_t)(j * kKsQuads + q) * 64 + (threadIdx.x & 63u));
+  }
   NT_D NT_INLINE void put(int j, const ge_p2& P, const fe& a) const {
     uint32_t w[40];
 #pragma unroll
@@ -154,11 +156,11 @@ hipError_t launch_verify_m(uint64_t blocks, const uint8_t* d_pk, const uint8_t* 
                            const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_combB,
                            void* d_ws, uint64_t* d_out_words, hipStream_t s);
 template <int MODE, int WA>
-hipError_t launch_keyset_m(uint64_t blocks, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
+hipError_t launch_keyset_m(const KsPlan& plan, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                            const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                            const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
                            const uint32_t* d_combB, void* d_stash, uint64_t* d_out_words, const uint32_t* d_perm,
-                           uint8_t* d_out_bytes, uint32_t per_lane, hipStream_t s);
+                           uint8_t* d_out_bytes, uint32_t* d_chunk_ctr, hipStream_t s);
 int keyset_occupancy();
 
 // Occupancy variants (waves per SIMD the register allocator targets), chosen

@@ -1,0 +1,60 @@
+// ks_plan.hpp -- launch plan of the key-cache verification kernel (host-only
+// arithmetic, shared by k_misc.hip and the host test harness).
+//
+// A launch of n signatures is R = ceil(n / 64) rows (one signature per lane of
+// a wave).  A lane verifies the rows of a chunk with ONE field inversion
+// (Montgomery's trick), so a chunk of p rows costs about A p + B multiply-
+// accumulates per lane (A = 16.66 k: the comb additions, SHA-512, compare;
+// B = 15.07 k: the inversion; profiles/opcount.json).  The plan launches a
+// persistent grid of `waves` waves (2 or 3 per SIMD) and cuts the rows into
+// chunks = k x waves chunks of `base_rows` or `base_rows + 1` rows (k = the
+// fewest rounds with at most `cap` rows per chunk), so every wave runs k
+// chunks of (nearly) equal size: no SIMD ends with a lone tail wave, which
+// the fixed 8-rows-per-wave grid of round 2 left at 4.32, 2.16, 1.08 and 0.54
+// rounds per launch for config 3 on 1, 2, 4 and 8 GPUs.
+// Between 2 and 3 waves per SIMD the plan takes the cheaper of
+//   k (A pmax + B) x (waves per SIMD) / T(waves per SIMD)
+// with T(2) = 0.97, T(3) = 1 (issue rate of 2 vs 3 resident waves, measured
+// on the key-cache kernel: profiles/r01/ab_occ_v9).
+#pragma once
+#include <stdint.h>
+
+namespace nt {
+
+struct KsPlan {
+  uint32_t waves;      // persistent waves launched (<= per_simd x 4 x cus)
+  uint32_t chunks;     // chunk indices claimed from the launch's counter
+  uint32_t base_rows;  // rows of a chunk; the first `extra` chunks have one more
+  uint32_t extra;
+  uint32_t per_simd;   // resident waves per SIMD the launch is sized for (2 or 3)
+  uint32_t rounds;     // k: chunks per wave
+};
+
+// force_per_simd: 0 = cheaper of 2 and 3, else 2 or 3; cap: most rows per chunk (1..8)
+inline KsPlan ks_plan(uint64_t n, uint32_t cus, uint32_t cap, int force_per_simd) {
+  const double A = 16.66, B = 15.07;
+  const uint64_t rows = (n + 63) / 64;
+  KsPlan best{0, 0, 0, 0, 2, 0};
+  double best_t = -1.0;
+  for (uint32_t w = 2; w <= 3; ++w) {
+    if (force_per_simd && (int)w != force_per_simd) continue;
+    const uint64_t slots = (uint64_t)w * 4 * (cus ? cus : 1);
+    const uint64_t W = rows < slots ? rows : slots;
+    if (W == 0) return KsPlan{0, 0, 0, 0, w, 0};
+    const uint64_t k = (rows + cap * W - 1) / (cap * W);
+    const uint64_t C = k * W < rows ? k * W : rows;  // cap 1: one row per chunk
+    const uint64_t base = rows / C, extra = rows % C;
+    const uint64_t pmax = base + (extra ? 1 : 0);
+    // waves per SIMD actually resident (a launch smaller than the slots fills fewer)
+    const uint64_t per = (W + 4 * (uint64_t)cus - 1) / (4 * (uint64_t)(cus ? cus : 1));
+    const double T = w == 2 ? 0.97 : 1.0;
+    const double t = (double)k * (A * (double)pmax + B) * (double)per / T;
+    if (best_t < 0 || t < best_t - 1e-9) {
+      best_t = t;
+      best = KsPlan{(uint32_t)W, (uint32_t)C, (uint32_t)base, (uint32_t)extra, w, (uint32_t)k};
+    }
+  }
+  return best;
+}
+
+}  // namespace nt

@@ -291,7 +291,7 @@ struct Device {
     DevBuf& st = k ? stash2 : d[B_STASH];
     DevBuf& so = k ? sort2 : d[B_SORT];
     const hipEvent_t ev = k ? stash2_done : stash_done;
-    const int rc = grow_synced(st, nt::keyset_stash_bytes(m), ev);
+    const int rc = grow_synced(st, nt::keyset_stash_bytes(m, cus), ev);
     return rc != NT_OK ? rc : grow_synced(so, nt::keyset_sort_bytes(m), ev);
   }
 
@@ -1080,7 +1080,7 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
           void* so = (c & 1) ? dv.sort2.p : dv.d[B_SORT].p;
           NT_CHK(dv.keyset_launch(s, st, [&] {
             return nt::launch_verify_keyset(NT_MODE_COFACTORLESS, ks->bits, (const uint32_t*)dk, dsig, dmsg, doff, dlen,
-                                            mc, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, st, so, dout, s);
+                                            mc, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, st, so, dout, dv.cus, s);
           }));
         } else {
           NT_CHK(dv.verify_chunk((int)c, NT_MODE_COFACTORLESS, dk, dsig, dmsg, doff, dlen, mc, dout));
@@ -1307,7 +1307,7 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
                                         dv.d[B_SIG].as<uint8_t>() + 64 * a, dv.d[B_DATA].as<uint8_t>(),
                                         dv.d[B_OFF].as<uint64_t>() + a, dv.d[B_LEN].as<uint64_t>() + a, b - a,
                                         pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, st, so,
-                                        dv.d[B_OUT].as<uint64_t>() + a / 64, s);
+                                        dv.d[B_OUT].as<uint64_t>() + a / 64, dv.cus, s);
       }));
     }
     NT_TRY(dv.join());
@@ -1394,7 +1394,7 @@ int nt_dev_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int dev, void
   void* so = k ? dv->sort2.p : dv->d[B_SORT].p;
   return dv->keyset_launch(s, stash, [&] {
     return nt::launch_verify_keyset(mode, ks->bits, d_key_idx, d_sig64, d_msg, d_off, d_len, n, pd.d_meta, pd.d_enc,
-                                    pd.d_comb, ks->nkeys, dv->d_combB, stash, so, d_out_words, s);
+                                    pd.d_comb, ks->nkeys, dv->d_combB, stash, so, d_out_words, dv->cus, s);
   });
 }
 

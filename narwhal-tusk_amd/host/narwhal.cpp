@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -377,25 +378,37 @@ std::vector<uint8_t> processor_message(const Processor& p, const crypto::Digest&
 }  // namespace
 
 // One side of the double buffer: the batches' bytes back to back in pinned
-// memory (nt_host_alloc), their offsets / lengths, and the waiting Processors.
+// memory (nt_host_alloc; ordinary memory if pinning fails -- the flush then
+// goes through the library's staging copy), their offsets / lengths, and the
+// waiting Processors.
 struct DigestBatcher::Queue {
   uint8_t* arena = nullptr;
+  bool pinned = false;
   size_t cap = 0, used = 0;
   std::vector<uint64_t> off, len;
   std::vector<Processor> procs;
   std::vector<std::promise<Output>> waiters;
   std::chrono::steady_clock::time_point oldest;
-  ~Queue() {
-    if (arena) nt_host_free(arena);
+  ~Queue() { release(arena, pinned); }
+  static void release(uint8_t* a, bool pin) {
+    if (!a) return;
+    if (pin) nt_host_free(a);
+    else std::free(a);
   }
   void reserve(size_t need) {
     if (need <= cap) return;
     size_t c = std::max<size_t>(need, std::max<size_t>(2 * cap, 1u << 20));
+    bool pin = true;
     auto* a = (uint8_t*)nt_host_alloc(c);
-    if (!a) throw crypto::BackendError("nt_host_alloc failed");
+    if (!a) {
+      pin = false;
+      a = (uint8_t*)std::malloc(c);
+    }
+    if (!a) throw std::bad_alloc();
     if (used) std::memcpy(a, arena, used);
-    if (arena) nt_host_free(arena);
+    release(arena, pinned);
     arena = a;
+    pinned = pin;
     cap = c;
   }
   void clear() {
@@ -490,27 +503,42 @@ void DigestBatcher::run() {
   }
 }
 
+// Runs on the flusher thread: every waiter of the taken queue is resolved,
+// with a digest or with an exception -- an exception that escaped here would
+// end the thread and with it the process (std::terminate), e.g. the
+// BackendError of a first nt_init that fails or a std::bad_alloc.
 void DigestBatcher::hash(Queue& q) {
   const size_t n = q.off.size();
-  std::vector<crypto::Digest> dig(n);
-  const auto t0 = std::chrono::steady_clock::now();
-  const int rc = nt_sha512_trunc32(crypto::Backend::global().ctx(), q.arena, q.off.data(), q.len.data(), n,
-                                   dig[0].bytes.data());
-  const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    stats_.flushes += 1;
-    stats_.batches += n;
-    stats_.bytes += q.used;
-    stats_.hash_seconds += dt;
-  }
-  for (size_t i = 0; i < n; ++i) {
-    if (rc != NT_OK) {  // a backend failure is an error for every waiter, never a digest
-      q.waiters[i].set_exception(std::make_exception_ptr(
-          crypto::BackendError(std::string("nt_sha512_trunc32 failed: ") + nt_strerror(rc))));
-      continue;
+  size_t done = 0;  // waiters resolved so far
+  try {
+    std::vector<crypto::Digest> dig(n);
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = nt_sha512_trunc32(crypto::Backend::global().ctx(), q.arena, q.off.data(), q.len.data(), n,
+                                     dig[0].bytes.data());
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stats_.flushes += 1;
+      stats_.batches += n;
+      stats_.bytes += q.used;
+      stats_.hash_seconds += dt;
     }
-    q.waiters[i].set_value(Output{dig[i], processor_message(q.procs[i], dig[i])});
+    for (; done < n; ++done) {
+      if (rc != NT_OK) {  // a backend failure is an error for every waiter, never a digest
+        q.waiters[done].set_exception(std::make_exception_ptr(
+            crypto::BackendError(std::string("nt_sha512_trunc32 failed: ") + nt_strerror(rc))));
+        continue;
+      }
+      q.waiters[done].set_value(Output{dig[done], processor_message(q.procs[done], dig[done])});
+    }
+  } catch (...) {
+    const std::exception_ptr ex = std::current_exception();
+    for (; done < n; ++done) {
+      try {
+        q.waiters[done].set_exception(ex);
+      } catch (...) {  // already satisfied: nothing left to tell this waiter
+      }
+    }
   }
 }
 

@@ -1,8 +1,10 @@
 """Subprocess helper of test_gpu_parity.test_keyset_per_lane_counts (not a test
 module): the corpus through the key cache in mixed mode with the per-lane
-signature count the parent chose (NT_KEYSET_PER_LANE, read once per process
-by libntcrypto), tiled to 72k signatures (key-grouped order) and as the plain
-corpus (input order).  Prints one JSON line: mismatches per launch."""
+row cap and waves per SIMD the parent chose (NT_KEYSET_PER_LANE,
+NT_KEYSET_WAVES, read once per process by libntcrypto), as the plain corpus
+(input order), tiled to 72k signatures (key-grouped order, one row per
+chunk) and to ~1M signatures (multi-row chunks, several rounds at small
+caps).  Prints one JSON line: mismatches per launch."""
 import json
 import os
 import sys
@@ -18,8 +20,8 @@ be = ntcrypto.Backend(0)
 uniq, inv = np.unique(d["pk"], axis=0, return_inverse=True)
 inv = inv.ravel().astype(np.uint32)
 ks = be.keyset(uniq)
-out = {"per_lane": os.environ.get("NT_KEYSET_PER_LANE")}
-for reps in (1, 200):
+out = {"per_lane": os.environ.get("NT_KEYSET_PER_LANE"), "waves": os.environ.get("NT_KEYSET_WAVES")}
+for reps in (1, 200, 2800):
     n0 = len(inv)
     idx = np.tile(inv, reps)
     unknown = (np.arange(n0 * reps) % 97) == 5

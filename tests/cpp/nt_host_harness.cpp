@@ -12,6 +12,7 @@
 #include <unordered_map>
 
 #include "../../narwhal-tusk_amd/csrc/ed25519_ops.hpp"
+#include "../../narwhal-tusk_amd/csrc/ks_plan.hpp"
 
 namespace nt {
 unsigned long long g_fe_mul = 0, g_fe_sq = 0;
@@ -367,4 +368,9 @@ void nth_counts_reset() { bcomb(); g_fe_mul = g_fe_sq = 0; }
 unsigned long long nth_count_mul() { return g_fe_mul; }
 unsigned long long nth_count_sq() { return g_fe_sq; }
 int nth_bcomb_bits() { return kBCombBits; }
+// the key-cache launch plan (ks_plan.hpp): out = waves, chunks, base_rows, extra, per_simd, rounds
+void nth_ks_plan(unsigned long long n, uint32_t cus, uint32_t cap, int force, uint32_t* out) {
+  const KsPlan p = ks_plan(n, cus, cap, force);
+  out[0] = p.waves; out[1] = p.chunks; out[2] = p.base_rows; out[3] = p.extra; out[4] = p.per_simd; out[5] = p.rounds;
+}
 }

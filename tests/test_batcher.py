@@ -101,3 +101,38 @@ def test_flush_rules():
         assert [b.wait(x)[0] for x in t] == [hashlib.sha512(y).digest()[:32] for y in ys]
     finally:
         b.close()
+
+
+_FAIL_PROBE = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+from ntcrypto import narwhal as N
+b = N.DigestBatcher(max_batches=2, max_delay_us=100)
+ok = 0
+for round_ in range(2):  # the flusher survives a failed flush and serves the next one
+    ts = [b.submit(0, True, bytes(1000)) for _ in range(3)]
+    for t in ts:
+        try:
+            b.wait(t)
+        except N.NtError:
+            ok += 1
+b.close()
+print("failed-waiters", ok)
+"""
+
+
+def test_backend_failure_reaches_every_waiter():
+    """ADVICE r02: a flush whose backend cannot start (Backend::global() throws
+    BackendError: here NT_DEVICE names a device that does not exist, so the
+    first nt_init_device fails) must fail each waiter's future -- not end the
+    flusher thread, and with it the process, in std::terminate.  Runs in a
+    subprocess (a regression would abort it) on CPU and GPU boxes alike."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, NT_DEVICE="97")
+    r = subprocess.run([sys.executable, "-c", _FAIL_PROBE, os.path.join(root, "narwhal-tusk_amd")], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
+    assert "failed-waiters 6" in r.stdout, r.stdout

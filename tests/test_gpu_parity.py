@@ -293,24 +293,32 @@ def test_keyset_committee_random_vs_oracle(be, oracle):
     ks.close()
 
 
+@pytest.mark.timeout(400)
 def test_keyset_per_lane_counts():
-    """The key-cache kernel's per-lane signature count is a kernel argument
-    (keyset_per_lane(): 8 by default, NT_KEYSET_PER_LANE for A/B runs, read once
-    per process): counts 1, 3 and 5 -- partial waves, other stash strides, other
-    inversion batch sizes -- give the corpus verdicts in input order and in
-    key-grouped order (subprocesses: the variable is read at first use)."""
+    """The key-cache kernel is a persistent grid claiming chunks of rows
+    (ks_plan.hpp: rounds x waves chunks of base or base + 1 rows, at most
+    NT_KEYSET_PER_LANE rows, 2 or 3 waves per SIMD by NT_KEYSET_WAVES or the
+    plan's cost model; both read once per process).  Caps 1, 3, 5 and 8 with
+    forced and automatic wave counts -- partial rows, other chunk sizes, several
+    rounds per wave, other inversion batch sizes -- give the corpus verdicts in
+    input order, in key-grouped order (72k) and at ~1M signatures (subprocesses:
+    the variables are read at first use)."""
     import json
     import subprocess
     import sys
     probe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_keyset_per_lane_probe.py")
-    for m in (1, 3, 5):
+    for m, w in ((1, ""), (3, "3"), (5, "2"), (8, "2"), (8, "3")):
         env = dict(os.environ, NT_KEYSET_PER_LANE=str(m), NT_KEYSET_COMB_BITS="16")
+        env.pop("NT_KEYSET_WAVES", None)
+        if w:
+            env["NT_KEYSET_WAVES"] = w
         r = subprocess.run([sys.executable, probe], env=env, capture_output=True, text=True, timeout=150)
         assert r.returncode == 0, r.stderr[-2000:]
         res = json.loads(r.stdout.strip().splitlines()[-1])
         assert res["per_lane"] == str(m)
         bad = {k: v for k, v in res.items() if k.startswith("mismatches") and v}
-        assert not bad, (m, bad)
+        assert not bad, (m, w, bad)
+        assert len([k for k in res if k.startswith("mismatches")]) == 3
 
 
 @pytest.mark.gpu
