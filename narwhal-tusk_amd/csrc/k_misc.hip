@@ -530,7 +530,10 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
       bytes = (uint8_t*)(p + m);
       const int mixed = mode == kMixed;
       if ((e = hipMemsetAsync(hist, 0, 4ull * (nkeys + 1), s)) != hipSuccess) return e;
-      const uint32_t hb = (uint32_t)((m + kBlock - 1) / kBlock < 2048 ? (m + kBlock - 1) / kBlock : 2048);
+      // ~64 keys per thread: every block flushes its LDS histogram with one global
+      // atomic per bucket, so fewer blocks = less contention on the nkeys + 1 counters
+      const uint64_t hw = (m + (uint64_t)kBlock * 64 - 1) / ((uint64_t)kBlock * 64);
+      const uint32_t hb = (uint32_t)(hw < 1024 ? hw : 1024);
       hipLaunchKernelGGL(k_key_hist, dim3(hb), dim3(kBlock), 0, s, d_key_idx + lo, m, mixed, nkeys, hist);
       hipLaunchKernelGGL(k_key_scan, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)hist, nkeys + 1, cursor);
       const uint64_t sb = (m + (uint64_t)kBlock * kSortTile - 1) / ((uint64_t)kBlock * kSortTile);

@@ -24,58 +24,11 @@
 #include "../../include/ntcrypto.h"
 #include "cpu_lane.hpp"
 #include "kernels.hpp"
+#include "runtime.hpp"
 
-namespace {
+namespace ntrt {
 
-#define NT_TRY(expr)                       \
-  do {                                     \
-    hipError_t _e = (expr);                \
-    if (_e != hipSuccess) return NT_EHIP;  \
-  } while (0)
-
-#define NT_CHK0(expr)             \
-  do {                            \
-    int _rc = (expr);             \
-    if (_rc != NT_OK) return _rc; \
-  } while (0)
-
-struct DevBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-  int ensure(size_t bytes) {
-    if (bytes <= cap) return NT_OK;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-    size_t want = std::max<size_t>(bytes, 1 << 16);
-    want = (want + 4095) & ~(size_t)4095;
-    if (hipMalloc(&p, want) != hipSuccess) return NT_ENOMEM;
-    cap = want;
-    return NT_OK;
-  }
-  template <class T>
-  T* as() const { return (T*)p; }
-};
-
-struct HostBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-  int ensure(size_t bytes) {
-    if (bytes <= cap) return NT_OK;
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    cap = 0;
-    size_t want = std::max<size_t>(bytes, 1 << 16);
-    want = (want + 4095) & ~(size_t)4095;
-    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return NT_ENOMEM;
-    cap = want;
-    return NT_OK;
-  }
-  template <class T>
-  T* as() const { return (T*)p; }
-};
-
-// nt_host_alloc registry: [base, base + bytes) of every live pinned buffer
+// nt_host_alloc registry (runtime.hpp)
 std::mutex g_pin_mu;
 std::map<uintptr_t, uint64_t> g_pinned;
 
@@ -87,284 +40,9 @@ bool is_pinned(const void* p, uint64_t bytes) {
   return (uintptr_t)p + bytes <= it->first + it->second;
 }
 
-enum { B_DATA, B_OFF, B_LEN, B_PK, B_SIG, B_OUT, B_OUT2, B_FIRST, B_CNT, B_STASH, B_SORT, B_NBUF };
+}  // namespace ntrt
 
-struct Device {
-  int ordinal = -1;
-  int group = -1;               // index of this device entry in nt_ctx::devs (keyset tables)
-  bool owns_comb = true;        // false for the extra slots (they share the entry's comb of B)
-  hipStream_t stream = nullptr;
-  uint32_t* d_combB = nullptr;  // wide comb of B (verify, key-cache verify, sign)
-  void* d_ws = nullptr;
-  uint32_t ws_slots = 0;
-  uint32_t sign_blocks = 0;
-  uint32_t cus = 0;
-  hipEvent_t ws_done = nullptr;  // orders every kernel that uses d_ws, whatever its stream
-  hipEvent_t stash_done = nullptr;  // same for the key-cache stash d[B_STASH] (host and device API)
-  // host entry points: chunk c's H2D copies go on cstream and chunk c's kernels
-  // wait for cev[c] on `stream`, so copies of chunk c+1 overlap kernels of chunk c
-  hipStream_t cstream = nullptr;
-  hipEvent_t cev[16] = {};
-  // ... and chunks alternate between two compute streams, so the waves of chunk
-  // c+1 fill the CUs that chunk c's last waves leave idle.  Stream 2 has its own
-  // verify workspace and key-cache stash.
-  hipStream_t stream2 = nullptr;
-  hipEvent_t join2 = nullptr, ws2_done = nullptr, stash2_done = nullptr;
-  DevBuf ws2, stash2, sort2;
-  std::mutex mu;
-  uint64_t dev_calls = 0;  // device-API verify calls (workspace alternation), under mu
-  uint64_t ks_calls = 0;   // device-API key-cache calls (stash alternation), under mu
-  DevBuf d[B_NBUF];
-  HostBuf h[B_NBUF];
-  // Extra execution slots of the same device entry (NT_SLOTS, default 2 in
-  // all): each has its own streams, workspace and staging and shares the comb
-  // of B, so a long call (a batch of digests) on one slot does not block a
-  // concurrent call (a certificate batch) on the device -- both run on the GPU
-  // at once.  Host entry points take the first free slot (SURVEY §8(b):
-  // "per-call stream acquisition from a pool").
-  std::vector<std::unique_ptr<Device>> extra;
-
-  ~Device() {
-    if (ordinal < 0) return;
-    (void)hipSetDevice(ordinal);
-    if (stream) (void)hipStreamSynchronize(stream);
-    for (auto& b : d)
-      if (b.p) (void)hipFree(b.p);
-    for (auto& b : h)
-      if (b.p) (void)hipHostFree(b.p);
-    extra.clear();  // before this entry's comb, which the extra slots borrow
-    (void)hipSetDevice(ordinal);
-    if (d_combB && owns_comb) (void)hipFree(d_combB);
-    if (d_ws) (void)hipFree(d_ws);
-    if (ws_done) (void)hipEventDestroy(ws_done);
-    if (stash_done) (void)hipEventDestroy(stash_done);
-    for (auto& e : cev)
-      if (e) (void)hipEventDestroy(e);
-    if (stream2 && stream2 != stream) (void)hipStreamSynchronize(stream2);
-    if (ws2.p) (void)hipFree(ws2.p);
-    if (stash2.p) (void)hipFree(stash2.p);
-    if (sort2.p) (void)hipFree(sort2.p);
-    if (join2) (void)hipEventDestroy(join2);
-    if (ws2_done) (void)hipEventDestroy(ws2_done);
-    if (stash2_done) (void)hipEventDestroy(stash2_done);
-    if (stream2 && stream2 != stream) (void)hipStreamDestroy(stream2);
-    if (cstream && cstream != stream) (void)hipStreamDestroy(cstream);
-    if (stream) (void)hipStreamDestroy(stream);
-  }
-
-  int init(int ord, int grp, const Device* share = nullptr) {
-    ordinal = ord;
-    group = grp;
-    NT_TRY(hipSetDevice(ord));
-    hipDeviceProp_t prop;
-    NT_TRY(hipGetDeviceProperties(&prop, ord));
-    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return NT_ENODEV;
-    if (share) {
-      // an extra (latency) slot: ONE stream at the highest priority for its
-      // copies and kernels, so it does not share a hardware queue with the
-      // bulk streams of the entry's first slot (HIP multiplexes a process's
-      // streams over GPU_MAX_HW_QUEUES = 4 queues; a kernel behind a 17 ms
-      // digest flush in the same queue waits for it)
-      int lo = 0, hi = 0;
-      NT_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      NT_TRY(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
-      cstream = stream2 = stream;
-    } else {
-      NT_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-      NT_TRY(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
-      NT_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
-    }
-    NT_TRY(hipEventCreateWithFlags(&ws_done, hipEventDisableTiming));
-    NT_TRY(hipEventCreateWithFlags(&stash_done, hipEventDisableTiming));
-    for (auto& e : cev) NT_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    NT_TRY(hipEventCreateWithFlags(&join2, hipEventDisableTiming));
-    NT_TRY(hipEventCreateWithFlags(&ws2_done, hipEventDisableTiming));
-    NT_TRY(hipEventCreateWithFlags(&stash2_done, hipEventDisableTiming));
-    if (share) {
-      d_combB = share->d_combB;
-      owns_comb = false;
-    } else {
-      static const uint32_t kB[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
-                                     0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
-      if (hipMalloc(&d_combB, nt::wcomb_bytes_per_key(nt::bcomb_bits())) != hipSuccess) return NT_ENOMEM;
-      NT_CHK0(build_wcombs(nt::bcomb_bits(), kB, 1, 0, d_combB, nullptr));
-    }
-    // Workspace slots = grid cap of the verify kernel.  Four times the resident
-    // workgroups (256-thread blocks, `occupancy` waves per SIMD, 4 SIMDs per CU):
-    // up to 2M signatures per launch the grid is then one 512-signature block per
-    // slot and the hardware dispatcher balances the tail (interleaved A/B on
-    // MI355X, tools/ab_env.sh: ~1% over 1x and 2x resident).
-    uint32_t slots = (uint32_t)prop.multiProcessorCount * (uint32_t)nt::verify_occupancy() * 4;
-    if (const char* e = std::getenv("NT_WS_SLOTS")) slots = (uint32_t)std::max(1, std::atoi(e));
-    ws_slots = slots;
-    sign_blocks = (uint32_t)prop.multiProcessorCount * 8;
-    cus = (uint32_t)prop.multiProcessorCount;
-    if (hipMalloc(&d_ws, nt::ws_bytes_per_slot() * ws_slots) != hipSuccess) return NT_ENOMEM;
-    NT_TRY(hipEventRecord(ws_done, stream));
-    NT_TRY(hipEventRecord(stash_done, stream));
-    NT_TRY(hipEventRecord(ws2_done, stream));
-    NT_TRY(hipEventRecord(stash2_done, stream));
-    NT_TRY(hipStreamSynchronize(stream));
-    return NT_OK;
-  }
-
-  // Wide combs of nkeys encoded points (host words) into d_comb (device);
-  // negate: comb of -P (committee keys) instead of P (the base point).
-  int build_wcombs(int bits, const uint32_t* enc_host, uint32_t nkeys, int negate, uint32_t* d_comb, uint32_t* d_meta) {
-    if (nkeys == 0) return NT_OK;
-    const uint32_t batch = std::min<uint32_t>(nkeys, nt::wcomb_fill_batch(bits));
-    uint32_t *d_enc = nullptr, *d_bases = nullptr, *d_tmp = nullptr;
-    int rc = NT_OK;
-    if (hipMalloc(&d_enc, 32ull * nkeys) != hipSuccess ||
-        hipMalloc(&d_bases, nt::wcomb_bases_bytes_per_key(bits) * nkeys) != hipSuccess ||
-        hipMalloc(&d_tmp, nt::wcomb_fill_tmp_bytes_per_key(bits) * batch) != hipSuccess) {
-      rc = NT_ENOMEM;
-    } else if (hipMemcpyAsync(d_enc, enc_host, 32ull * nkeys, hipMemcpyHostToDevice, stream) != hipSuccess ||
-               nt::launch_wcomb_build(bits, d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, stream) !=
-                   hipSuccess ||
-               hipStreamSynchronize(stream) != hipSuccess) {
-      rc = NT_EHIP;
-    }
-    if (d_enc) (void)hipFree(d_enc);
-    if (d_bases) (void)hipFree(d_bases);
-    if (d_tmp) (void)hipFree(d_tmp);
-    return rc;
-  }
-
-  // compute stream of chunk c
-  hipStream_t cstr(int c) const { return (c & 1) ? stream2 : stream; }
-
-  // the kernels of chunk c wait for the copies issued so far on cstream
-  hipError_t fence(int c) {
-    hipError_t e = hipEventRecord(cev[c], cstream);
-    if (e != hipSuccess) return e;
-    return hipStreamWaitEvent(cstr(c), cev[c], 0);
-  }
-
-  // `stream` waits for everything issued on stream2
-  hipError_t join() {
-    hipError_t e = hipEventRecord(join2, stream2);
-    if (e != hipSuccess) return e;
-    return hipStreamWaitEvent(stream, join2, 0);
-  }
-
-  // verify launch of chunk c: even chunks use the device workspace on `stream`,
-  // odd chunks stream2's own workspace (grown to the chunk's grid)
-  int verify_chunk(int c, int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
-                   const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out) {
-    if (!(c & 1)) return verify(mode, pk, sig, msg, off, len, n, out, stream) == hipSuccess ? NT_OK : NT_EHIP;
-    const uint64_t blocks = nt::verify_grid(n, ws_slots);
-    const int rc = grow_ws2(blocks);
-    if (rc != NT_OK) return rc;
-    if (hipStreamWaitEvent(stream2, ws2_done, 0) != hipSuccess ||
-        nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, ws2.p, (uint32_t)std::max<uint64_t>(blocks, 1),
-                          out, stream2) != hipSuccess ||
-        hipEventRecord(ws2_done, stream2) != hipSuccess)
-      return NT_EHIP;
-    return NT_OK;
-  }
-
-  // Key-cache launch on stream s with stash st: every launch waits for the
-  // previous user of its stash (d[B_STASH]: stash_done, stash2: stash2_done --
-  // host chunks on `stream` / stream2 and device-API calls on any stream) and
-  // marks it, like the [k]A workspaces.  The key-grouping scratch (d[B_SORT] /
-  // sort2) goes with its stash.
-  template <class F>
-  int keyset_launch(hipStream_t s, void* st, F&& launch) {
-    const hipEvent_t ev = st == d[B_STASH].p ? stash_done : (st == stash2.p ? stash2_done : nullptr);
-    if (ev && hipStreamWaitEvent(s, ev, 0) != hipSuccess) return NT_EHIP;
-    if (launch() != hipSuccess) return NT_EHIP;
-    if (ev && hipEventRecord(ev, s) != hipSuccess) return NT_EHIP;
-    return NT_OK;
-  }
-
-  // Grow a buffer that enqueue-only device-API calls may still be using: wait
-  // for its last user (the launch that recorded ev) before freeing it.
-  int grow_synced(DevBuf& b, size_t bytes, hipEvent_t ev) {
-    if (bytes <= b.cap) return NT_OK;
-    if (b.p && hipEventSynchronize(ev) != hipSuccess) return NT_EHIP;
-    return b.ensure(bytes);
-  }
-  // the stash / key-grouping scratch pair of slot k (0: d[B_STASH] / d[B_SORT],
-  // 1: stash2 / sort2) for launches of up to m signatures
-  int ensure_stash(int k, uint64_t m) {
-    DevBuf& st = k ? stash2 : d[B_STASH];
-    DevBuf& so = k ? sort2 : d[B_SORT];
-    const hipEvent_t ev = k ? stash2_done : stash_done;
-    const int rc = grow_synced(st, nt::keyset_stash_bytes(m, cus), ev);
-    return rc != NT_OK ? rc : grow_synced(so, nt::keyset_sort_bytes(m), ev);
-  }
-
-  // ws2 holds >= blocks workspace slots; a grown buffer is freed only after its
-  // last user (the kernel that recorded ws2_done) has finished
-  int grow_ws2(uint64_t blocks) {
-    const size_t need = nt::ws_bytes_per_slot() * std::max<uint64_t>(blocks, 1);
-    if (need <= ws2.cap) return NT_OK;
-    if (ws2.p && hipEventSynchronize(ws2_done) != hipSuccess) return NT_EHIP;
-    return ws2.ensure(need);
-  }
-
-  // Device-API verify (nt_dev_ed25519_verify): successive calls alternate between
-  // the two workspaces, each ordered by its own event, so back-to-back batches
-  // issued on two caller streams overlap -- the waves of the next batch fill the
-  // SIMDs the previous batch's last round leaves idle.  Calls on one stream stay
-  // in stream order.  (Caller holds mu.)
-  hipError_t verify_dev(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
-                        const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out, hipStream_t s) {
-    if ((dev_calls++ & 1u) == 0) return verify(mode, pk, sig, msg, off, len, n, out, s);
-    if (grow_ws2(ws_slots) != NT_OK) return hipErrorOutOfMemory;
-    hipError_t e = hipStreamWaitEvent(s, ws2_done, 0);
-    if (e != hipSuccess) return e;
-    e = nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, ws2.p, ws_slots, out, s);
-    if (e != hipSuccess) return e;
-    return hipEventRecord(ws2_done, s);
-  }
-
-  // verify launch that shares the workspace: wait for the previous user, then mark
-  hipError_t verify(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
-                    const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out,
-                    hipStream_t s) {
-    hipError_t e = hipStreamWaitEvent(s, ws_done, 0);
-    if (e != hipSuccess) return e;
-    e = nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, d_ws, ws_slots, out, s);
-    if (e != hipSuccess) return e;
-    return hipEventRecord(ws_done, s);
-  }
-};
-
-}  // namespace
-
-struct nt_ctx {
-  std::vector<std::unique_ptr<Device>> devs;
-  // small-call path (cpu_lane.hpp): NT_SMALL_OFF / AUTO / ALWAYS, host threads
-  std::atomic<int> small_mode{NT_SMALL_OFF};
-  std::atomic<int> small_threads{1};
-  std::atomic<uint64_t> calls_host{0}, calls_gpu{0};
-};
-
-struct nt_keyset {
-  nt_ctx* ctx = nullptr;
-  uint32_t nkeys = 0;
-  std::vector<uint8_t> enc;     // host copy of the key encodings (small-call path)
-  int bits = 0;                 // comb digit width of every key (nt::kKeyComb{Wide,Mid,Narrow})
-  std::vector<uint32_t> flags;  // host copy of kKey* bits
-  struct PerDev {
-    int ordinal = -1;
-    uint32_t* d_enc = nullptr;
-    uint32_t* d_meta = nullptr;
-    uint32_t* d_comb = nullptr;
-  };
-  std::vector<PerDev> dev;
-  ~nt_keyset() {
-    for (auto& d : dev) {
-      if (d.ordinal < 0) continue;
-      (void)hipSetDevice(d.ordinal);
-      if (d.d_enc) (void)hipFree(d.d_enc);
-      if (d.d_meta) (void)hipFree(d.d_meta);
-      if (d.d_comb) (void)hipFree(d.d_comb);
-    }
-  }
-};
+using namespace ntrt;
 
 extern "C" {
 
@@ -475,90 +153,6 @@ void nt_host_free(void* p) {
 }  // extern "C"
 
 namespace {
-
-// Split [0, n) into one contiguous range per device, boundaries multiple of `align`.
-std::vector<std::pair<uint64_t, uint64_t>> shard(uint64_t n, size_t ndev, uint64_t align) {
-  std::vector<std::pair<uint64_t, uint64_t>> r;
-  uint64_t per = (n + ndev - 1) / ndev;
-  per = (per + align - 1) / align * align;
-  uint64_t lo = 0;
-  for (size_t d = 0; d < ndev; ++d) {
-    const uint64_t hi = std::min(n, lo + per);
-    r.emplace_back(lo, hi);
-    lo = hi;
-  }
-  return r;
-}
-
-// A free execution slot of device entry d, locked into lk.  Latency-sized
-// calls try the extra (high-priority) slots first, bulk calls the entry's own
-// slot first; when every slot is busy, wait for the preferred one.
-Device& acquire_slot(nt_ctx* ctx, size_t d, bool latency, std::unique_lock<std::mutex>& lk) {
-  Device& p = *ctx->devs[d];
-  std::vector<Device*> order;
-  if (!latency) order.push_back(&p);
-  for (auto& x : p.extra) order.push_back(x.get());
-  if (latency) order.push_back(&p);
-  for (Device* s : order) {
-    std::unique_lock<std::mutex> l(s->mu, std::try_to_lock);
-    if (l.owns_lock()) {
-      lk = std::move(l);
-      return *s;
-    }
-  }
-  lk = std::unique_lock<std::mutex>(order[0]->mu);
-  return *order[0];
-}
-
-// digests whose longest message is short (header / vote / certificate
-// preimages) finish fast; long ones (worker batches) are bulk
-bool sha_latency(uint64_t n, const uint64_t* len) {
-  for (uint64_t i = 0; i < n; ++i)
-    if (len[i] > (64u << 10)) return false;
-  return true;
-}
-
-// work below one round of resident waves: a latency-sized call
-bool latency_sized(const nt_ctx* ctx, uint64_t items_per_device, uint64_t round) {
-  (void)ctx;
-  return items_per_device <= round;
-}
-
-template <class F>
-int run_sharded(nt_ctx* ctx, uint64_t n, uint64_t align, F&& fn, bool latency = false) {
-  const size_t nd = ctx->devs.size();
-  auto parts = shard(n, nd, align);
-  if (nd == 1) {
-    std::unique_lock<std::mutex> lk;
-    Device& dv = acquire_slot(ctx, 0, latency, lk);
-    if (hipSetDevice(dv.ordinal) != hipSuccess) return NT_EHIP;
-    return fn(dv, parts[0].first, parts[0].second);
-  }
-  std::vector<int> rcs(nd, NT_OK);
-  std::vector<std::thread> th;
-  for (size_t d = 0; d < nd; ++d) {
-    if (parts[d].first >= parts[d].second) continue;
-    th.emplace_back([&, d] {
-      std::unique_lock<std::mutex> lk;
-      Device& dv = acquire_slot(ctx, d, latency, lk);
-      if (hipSetDevice(dv.ordinal) != hipSuccess) {
-        rcs[d] = NT_EHIP;
-        return;
-      }
-      rcs[d] = fn(dv, parts[d].first, parts[d].second);
-    });
-  }
-  for (auto& t : th) t.join();
-  for (int rc : rcs)
-    if (rc != NT_OK) return rc;
-  return NT_OK;
-}
-
-#define NT_CHK(expr)              \
-  do {                            \
-    int _rc = (expr);             \
-    if (_rc != NT_OK) return _rc; \
-  } while (0)
 
 // Stage the message span used by items [lo, hi) (rebased offsets, 16-B phase kept).
 int stage_messages(Device& dv, const uint8_t* data, const uint64_t* off, const uint64_t* len,
