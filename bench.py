@@ -1259,10 +1259,33 @@ def bench_ingest(args, be, world, rank, local, max_over_ranks, barrier):
             gotp = core.ingest_pipelined(data, off, ln, args.ingest_threads, chunk)
         wall = max_over_ranks(time.perf_counter() - t0)
         got = np.where(got == gotp, got, -1)
+        # certificates parsed and checked on the GPU from the wire bytes
+        # (Core::ingest_device -> nt_certificates_ingest): the bytes as received,
+        # in pinned memory (a receiver that owns its buffers), DMA'd per chunk
+        pdata = be.pinned(data.shape)
+        pdata[...] = data
+        core.ingest(pdata, off, ln, args.ingest_threads, device=True)   # warm-up (committee tables, buffers)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            gotd, host_n = core.ingest(pdata, off, ln, args.ingest_threads, device=True)
+        walld = max_over_ranks(time.perf_counter() - t0)
+        gotdp, _ = core.ingest(data, off, ln, args.ingest_threads, device=True)  # pageable input, once
+        del pdata
     finally:
         core.close()
     mism = int(max_over_ranks(int((got != expect).sum())))
-    return {"value": round(args.certs * steps / wall, 1), "unit": "certificates/s",
+    mismd = int(max_over_ranks(int((gotd != expect).sum()) + int((gotdp != expect).sum())))
+    device = {"certs_per_s": round(args.certs * steps / walld, 1), "ms_per_step": round(walld * 1e3 / steps, 3),
+              "host_decided": int(host_n), "mismatches_vs_expected": mismd,
+              "note": "Core::ingest_device: wire bytes copied as-is (pinned), parsed / checked on the GPU "
+                      "(k_cert_parse, k_cert_scatter, one SHA-512 + one NT_MODE_MIXED key-cache launch + group AND "
+                      "per chunk of %s messages, chunks alternating two streams so the PCIe copy of one runs under "
+                      "the previous one's kernels); PCIe-inclusive" % os.environ.get("NT_INGEST_CHUNK", "25000")}
+    return {"value": device["certs_per_s"], "unit": "certificates/s",
+            "path": "device parse (Core::ingest_device); host_decode = the host decoder path",
+            "device_parse": device,
+            "host_decode": {"certs_per_s": round(args.certs * steps / wall, 1)},
             "workload": "cfg3 as wire bytes: %d bincode PrimaryMessage::Certificate messages of %d B (n=%d "
                         "committee, %d votes), Core::ingest -> DagError per message" % (args.certs, wlen, nk, quorum),
             "ms_per_step": round(wall * 1e3 / steps, 3), "pipeline_chunk": chunk,

@@ -139,6 +139,45 @@ int nt_ed25519_verify_batch_groups_keyset(nt_ctx *ctx, const nt_keyset *ks, cons
                                           const uint32_t *cnt, const uint8_t *msg32, uint64_t G,
                                           uint8_t *out_group_bitmap, uint8_t *out_sig_bitmap);
 
+/* ---- certificate ingestion from wire bytes --------------
+ * The primary's receiver deserializes every PrimaryMessage with bincode
+ * (primary/src/primary.rs:225-244) before Core::sanitize_certificate
+ * (core.rs:339-346) runs Certificate::verify (messages.rs:189-215).  These
+ * entry points take the message bytes as they arrived, copy them to the
+ * device as-is and parse, check and verify them there: one SHA-512 launch
+ * (header ids and certificate digests), one NT_MODE_MIXED key-cache launch
+ * (the header signature strict, the votes cofactorless) and a group AND per
+ * chunk of messages, chunks pipelined so the PCIe copy of one overlaps the
+ * kernels of the previous one.
+ *
+ * nt_committee: the committee of a keyset (key i = keyset key i): stake per
+ * key, its worker ids (worker_ids[worker_first[i] .. worker_first[i + 1]),
+ * any order) and the quorum threshold (config/src/lib.rs:168-173:
+ * 2 * total_stake / 3 + 1).  Keys are looked up by their canonical base64
+ * text (crypto/src/lib.rs:73-79,103-112), as the reference's serde does. */
+typedef struct nt_committee nt_committee;
+int nt_committee_create(nt_ctx *ctx, const nt_keyset *ks, const uint32_t *stake, const uint64_t *worker_first,
+                        const uint32_t *worker_ids, uint32_t quorum, nt_committee **out);
+void nt_committee_free(nt_committee *cm);
+/* primary::DagError codes of out_code (host/narwhal.hpp; error.rs variants) */
+#define NT_DAG_OK 0
+#define NT_DAG_INVALID_SIGNATURE 1
+#define NT_DAG_INVALID_HEADER_ID 2
+#define NT_DAG_MALFORMED_HEADER 3
+#define NT_DAG_UNKNOWN_AUTHORITY 4
+#define NT_DAG_AUTHORITY_REUSE 5
+#define NT_DAG_REQUIRES_QUORUM 6
+#define NT_DAG_TOO_OLD 7
+/* a message this path does not decide: not a Certificate, not in canonical
+ * form (map / set entries out of order, a key string that is not a committee
+ * key's canonical base64 text), malformed or truncated -- the caller runs its
+ * host decoder on it (the C++ mirror: Core::ingest) */
+#define NT_DAG_HOST 0xff
+/* message i = data[off[i] .. off[i] + len[i]); out_code: n bytes.  Inputs in
+ * nt_host_alloc memory are DMA'd straight from it. */
+int nt_certificates_ingest(nt_ctx *ctx, const nt_committee *cm, const uint8_t *data, const uint64_t *off,
+                           const uint64_t *len, uint64_t n, uint64_t gc_round, uint8_t *out_code);
+
 /* ---- small-call path (SURVEY.md H3, §8(b) "CPU-fallback threshold") ------
  * The reference calls verify once per header / vote, verify_batch once per
  * certificate (primary/src/core.rs:349-411) and hashes one ~508 KB batch per

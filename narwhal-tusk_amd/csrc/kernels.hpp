@@ -52,4 +52,43 @@ int bcomb_bits();                     // digit width of the base-point comb
 size_t ws_bytes_per_slot();
 int verify_occupancy();  // waves per SIMD of the selected verify kernel variant
 
+// ---- certificate ingestion on the device (k_ingest.hip, ingest_gpu.cpp) ----
+// Committee tables of an nt_committee on one device.
+struct CertCommittee {
+  const uint32_t* enc;        // [nkeys][12]: canonical base64 text of the key (44 chars) + 4 zero bytes
+  const uint64_t* slot_head;  // [1 << sbits]: first 8 characters of the key in the slot
+  const uint32_t* slot_idx;   // [1 << sbits]: key index, 0xffffffff = empty (open addressing)
+  const uint32_t* stake;      // [nkeys]
+  const uint32_t* wfirst;     // [nkeys + 1]: key k's workers are wids[wfirst[k] .. wfirst[k + 1]), sorted
+  const uint32_t* wids;
+  const uint32_t* raw;        // [nkeys][8]: the raw 32-byte keys (the keyset's encodings)
+  uint32_t nkeys, sbits, quorum;
+};
+// One chunk of n messages: inputs, per-message state, launch buffers, outputs.
+struct CertBufs {
+  const uint8_t* wire;   // message bytes (64 bytes of readable slack on both sides)
+  const uint64_t* moff;  // message i = wire[moff[i] .. moff[i] + mlen[i])
+  const uint64_t* mlen;
+  uint64_t n;
+  uint64_t* round;       // k_cert_parse
+  uint32_t *author, *np, *nq, *nv, *flags, *plen;
+  uint64_t *vbase, *pbase;  // k_cert_scan (n + 1 entries)
+  uint8_t* mbase;        // [claimed ids 32 n][digests 64 n][certificate preimages 72 n][header preimages]
+  uint64_t pre_off;      // offset of the header preimages in mbase
+  uint32_t* keys;        // n + V key-cache launch entries: key index (| strict bit), signature, message
+  uint4* sigs;
+  uint64_t *smoff, *smlen;
+  uint64_t *soff, *slen;   // 2 n SHA-512 inputs (offsets into mbase)
+  uint64_t* gfirst;        // n vote groups
+  uint32_t* gcnt;
+  uint32_t *verr, *weight;
+  const uint64_t* sig_words;  // verdict words of the key-cache launch
+  const uint64_t* grp_words;  // group AND words
+  uint8_t* code;              // per message: primary::DagError, 0xff = host decoder
+};
+hipError_t launch_cert_parse(const CertCommittee& c, const CertBufs& b, hipStream_t s);
+hipError_t launch_cert_scan(const CertBufs& b, hipStream_t s);
+hipError_t launch_cert_scatter(const CertCommittee& c, const CertBufs& b, hipStream_t s);
+hipError_t launch_cert_verdict(const CertCommittee& c, const CertBufs& b, uint64_t gc_round, hipStream_t s);
+
 }  // namespace nt

@@ -110,6 +110,8 @@ struct Device {
   // at once.  Host entry points take the first free slot (SURVEY §8(b):
   // "per-call stream acquisition from a pool").
   std::vector<std::unique_ptr<Device>> extra;
+  // state of the wire-ingestion entry point on this slot (ingest_gpu.cpp), created on first use
+  std::shared_ptr<void> ingest;
 
   ~Device() {
     if (ordinal < 0) return;

@@ -83,13 +83,22 @@ void ntn_core_free(void* p) { delete (CoreHandle*)p; }
 
 // Core::ingest over n packed wire messages: out_codes[i] = primary::DagError.
 // Returns 0, or -2 on a backend failure (never reported as a verdict).
-// general = 1: the object-model decoder + sanitize_batch (cross-check path).
+// general = 1: the object-model decoder + sanitize_batch (cross-check path);
+// general = 2: Core::ingest_device (certificates parsed on the GPU), and
+// decode_seconds then returns the count of messages left to the host decoder.
 int ntn_core_ingest(void* p, const uint8_t* data, const uint64_t* off, const uint64_t* len, uint64_t n,
                     int threads, int32_t* out_codes, double* decode_seconds, int general) {
   try {
     const auto& core = ((CoreHandle*)p)->core;
-    const auto r = general ? core.ingest_general(data, off, len, (size_t)n, threads, decode_seconds)
-                           : core.ingest(data, off, len, (size_t)n, threads, decode_seconds);
+    std::vector<primary::DagError> r;
+    if (general == 2) {
+      size_t host = 0;
+      r = core.ingest_device(data, off, len, (size_t)n, threads, &host);
+      if (decode_seconds) *decode_seconds = (double)host;  // mode 2: messages left to the host decoder
+    } else {
+      r = general ? core.ingest_general(data, off, len, (size_t)n, threads, decode_seconds)
+                  : core.ingest(data, off, len, (size_t)n, threads, decode_seconds);
+    }
     for (uint64_t i = 0; i < n; ++i) out_codes[i] = (int32_t)r[i];
     return 0;
   } catch (const std::exception&) {

@@ -594,6 +594,55 @@ std::vector<DagError> Core::ingest_soa(const uint8_t* data, const uint64_t* off,
   return res;  // a copy: the workspace keeps its buffers
 }
 
+// The committee on the device (nt_committee) for ingest_device: built once per
+// Core from its committee and key cache (same key order: the committee map's).
+struct DeviceCommittee {
+  nt_committee* cm = nullptr;
+  ~DeviceCommittee() { nt_committee_free(cm); }
+};
+
+std::vector<DagError> Core::ingest_device(const uint8_t* data, const uint64_t* off, const uint64_t* len, size_t n,
+                                          int threads, size_t* host_decided) const {
+  if (!cache) throw crypto::BackendError("Core::ingest_device needs the committee key cache");
+  nt_ctx* ctx = crypto::Backend::global().ctx();
+  if (!dev_committee) {
+    const Committee& cm = *committee;
+    std::vector<uint32_t> stake, wids;
+    std::vector<uint64_t> wfirst{0};
+    for (const auto& kv : cm.authorities) {
+      stake.push_back(kv.second.stake);
+      wids.insert(wids.end(), kv.second.workers.begin(), kv.second.workers.end());
+      wfirst.push_back(wids.size());
+    }
+    auto d = std::make_shared<DeviceCommittee>();
+    check(nt_committee_create(ctx, cache->handle(), stake.data(), wfirst.data(), wids.data(), cm.quorum_threshold(),
+                              &d->cm),
+          "nt_committee_create");
+    dev_committee = d;
+  }
+  std::vector<uint8_t> code(std::max<size_t>(n, 1));
+  if (n) check(nt_certificates_ingest(ctx, dev_committee->cm, data, off, len, n, gc_round, code.data()),
+               "nt_certificates_ingest");
+  std::vector<DagError> res(n, DagError::Ok);
+  std::vector<uint64_t> hoff, hlen;
+  std::vector<size_t> hidx;
+  for (size_t i = 0; i < n; ++i) {
+    if (code[i] == NT_DAG_HOST) {
+      hidx.push_back(i);
+      hoff.push_back(off[i]);
+      hlen.push_back(len[i]);
+    } else {
+      res[i] = (DagError)code[i];
+    }
+  }
+  if (host_decided) *host_decided = hidx.size();
+  if (!hidx.empty()) {
+    const auto r = ingest_soa(data, hoff.data(), hlen.data(), hidx.size(), threads);
+    for (size_t k = 0; k < hidx.size(); ++k) res[hidx[k]] = r[k];
+  }
+  return res;
+}
+
 std::vector<DagError> Core::ingest_pipelined(const uint8_t* data, const uint64_t* off, const uint64_t* len,
                                              size_t n, int threads, size_t chunk) const {
   if (chunk == 0 || chunk >= n) return ingest_soa(data, off, len, n, threads);

@@ -115,6 +115,7 @@ std::unique_ptr<crypto::KeySet> committee_keyset(const Committee& committee);
 
 struct PrimaryMessage;  // wire.hpp
 struct IngestWorkspace;  // ingest.cpp
+struct DeviceCommittee;  // ingest.cpp: the nt_committee of a Core's committee + key cache
 
 // Phase times (seconds) of this thread's last Core::ingest (SoA path).
 struct IngestStats {
@@ -137,6 +138,7 @@ struct Core {
   // staging reused across ingest calls (one ingest at a time per Core, like the
   // reference's single Core task)
   mutable std::shared_ptr<IngestWorkspace> ws, ws_alt;
+  mutable std::shared_ptr<DeviceCommittee> dev_committee;
 
   std::vector<DagError> sanitize_batch(const std::vector<PrimaryMessage>& msgs) const;
   // wire ingestion (§8(f).2): bincode bytes of n PrimaryMessages (packed, off/len).
@@ -153,6 +155,12 @@ struct Core {
                                    int threads = 1, double* decode_seconds = nullptr) const;
   std::vector<DagError> ingest_general(const uint8_t* data, const uint64_t* off, const uint64_t* len, size_t n,
                                        int threads = 1, double* decode_seconds = nullptr) const;
+  // ingest_device: certificates parsed and checked on the GPU from the wire
+  // bytes (nt_certificates_ingest; needs the key cache); the messages that path
+  // leaves to the host (NT_DAG_HOST: other kinds, non-canonical or malformed
+  // bytes) go through ingest_soa.  Same verdicts as ingest.
+  std::vector<DagError> ingest_device(const uint8_t* data, const uint64_t* off, const uint64_t* len, size_t n,
+                                      int threads = 1, size_t* host_decided = nullptr) const;
   // the batch in chunks of `chunk` messages, two chunks in flight on two
   // workspaces: one chunk's host decode and checks overlap the other's GPU
   // launches.  Same verdicts as ingest (messages are independent).

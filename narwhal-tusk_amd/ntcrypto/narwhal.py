@@ -115,9 +115,12 @@ class Core:
         if not self._h:
             raise NtError("ntn_core_new failed (no gfx950 device, or a bad current header)")
 
-    def ingest(self, data, off, ln, threads=8, general=False):
+    def ingest(self, data, off, ln, threads=8, general=False, device=False):
         """DagError codes for n packed wire messages; also returns the host decode
-        seconds.  general=True: the object-model decoder (cross-check path)."""
+        seconds.  general=True: the object-model decoder (cross-check path).
+        device=True: Core::ingest_device -- certificates parsed and checked on the
+        GPU from the wire bytes (nt_certificates_ingest), the rest on the host;
+        the second value is then the count of messages the host decided."""
         n = len(off)
         codes = np.zeros(max(n, 1), np.int32)
         dec = ctypes.c_double(0)
@@ -127,10 +130,10 @@ class Core:
         rc = load().ntn_core_ingest(self._h, data.ctypes.data_as(_u8p), off.ctypes.data_as(_u64p),
                                     ln.ctypes.data_as(_u64p), n, threads,
                                     codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ctypes.byref(dec),
-                                    int(general))
+                                    2 if device else int(general))
         if rc != 0:
             raise NtError("ntn_core_ingest: backend failure")
-        return codes[:n], dec.value
+        return codes[:n], (int(dec.value) if device else dec.value)
 
     def ingest_pipelined(self, data, off, ln, threads=8, chunk=25000):
         """Core::ingest_pipelined: chunks of `chunk` messages, two in flight"""

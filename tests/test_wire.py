@@ -111,7 +111,7 @@ def test_wire_rejects_malformed():
 
 
 # ------------------------------------------------------------------ GPU: batched Core
-def _scenario(orc, rng):
+def _scenario(orc, rng, with_objs=False):
     seeds = [bytes([i + 1]) * 32 for i in range(7)]
     keys = [orc.pubkey(s) for s in seeds]
     sk = dict(zip(keys, seeds))
@@ -186,6 +186,8 @@ def _scenario(orc, rng):
     batch = lambda d, votes: orc.verify_batch([v[0] for v in votes], [v[1] for v in votes], d)
     expect = [W.model_sanitize(com, gc_round, cur, o, strict, batch) if o is not None else W.SERIALIZATION_ERROR
               for o in objs]
+    if with_objs:
+        return keys, stakes, nworkers, gc_round, cur, wires, expect, objs
     return keys, stakes, nworkers, gc_round, cur, wires, expect
 
 
@@ -195,7 +197,7 @@ def test_core_ingest_matches_model(use_keyset):
     from _oracle import load
     orc = load()
     rng = random.Random(2024)
-    keys, stakes, nworkers, gc_round, cur, wires, expect = _scenario(orc, rng)
+    keys, stakes, nworkers, gc_round, cur, wires, expect, objs = _scenario(orc, rng, with_objs=True)
     # every outcome is exercised
     assert set(expect) == set(range(11))
     core = N.Core(np.frombuffer(b"".join(keys), np.uint8), stakes, nworkers, gc_round, W.message(cur), use_keyset)
@@ -206,6 +208,13 @@ def test_core_ingest_matches_model(use_keyset):
             assert [names[c] for c in got] == [names[c] for c in expect], general
         got = core.ingest_pipelined(*N.pack(wires), threads=2, chunk=5)  # two chunks in flight
         assert [names[c] for c in got] == [names[c] for c in expect]
+        if use_keyset:
+            # certificates parsed and checked on the GPU (nt_certificates_ingest), the
+            # rest (headers, votes, a request, garbage, non-canonical bytes) on the host
+            got, host = core.ingest(*N.pack(wires), threads=3, device=True)
+            assert [names[c] for c in got] == [names[c] for c in expect]
+            ncert = sum(isinstance(o, W.Certificate) for o in objs)
+            assert host <= len(wires) - ncert + 1  # every canonical certificate decided on the device
         # the same messages one at a time give the same verdicts
         for w, e in zip(wires, expect):
             g, _ = core.ingest(*N.pack([w]), threads=1)
@@ -289,6 +298,74 @@ def test_core_soa_vs_general_fuzz():
         b, _ = core.ingest(*N.pack(batch), threads=4, general=True)
         assert np.array_equal(a, b), [(i, N.DAG_ERRORS[x], N.DAG_ERRORS[y]) for i, (x, y) in enumerate(zip(a, b))
                                       if x != y][:10]
+        c, host = core.ingest(*N.pack(batch), threads=4, device=True)  # GPU wire parsing
+        assert np.array_equal(a, c), [(i, N.DAG_ERRORS[x], N.DAG_ERRORS[y]) for i, (x, y) in enumerate(zip(a, c))
+                                      if x != y][:10]
+        assert host < len(batch)
         assert len(set(a.tolist())) >= 6
+    finally:
+        core.close()
+
+
+def _cert_batch(orc, rng, nk, G, quorum):
+    """G certificates of an nk-key committee as wire bytes, with a mix of
+    corruptions in the bytes the device parser reads: signatures, header ids,
+    payload / parent order, worker ids, vote keys, counts, truncations."""
+    seeds = [bytes([i + 1, 7]) * 16 for i in range(nk)]
+    keys = [orc.pubkey(s) for s in seeds]
+    sk = dict(zip(keys, seeds))
+    wires = []
+    for g in range(G):
+        author = keys[rng.randrange(nk)]
+        h = W.Header(author, 10 + rng.randrange(5), {_rb(rng, 32): rng.randrange(2) for _ in range(rng.randrange(0, 6))},
+                     {_rb(rng, 32) for _ in range(rng.randrange(0, 5))})
+        h.sig = orc.sign(sk[author], author, h.id)
+        c = W.Certificate(h, [])
+        d = c.digest()
+        for pk in rng.sample(keys, quorum + rng.randrange(0, 2)):
+            c.votes.append((pk, orc.sign(sk[pk], pk, d)))
+        m = bytearray(W.message(c))
+        k = g % 10
+        if k == 1:                                   # a vote signature
+            m[-1 - rng.randrange(64)] ^= 1 << rng.randrange(8)
+        elif k == 2:                                 # anything
+            m[rng.randrange(len(m))] ^= 1 << rng.randrange(8)
+        elif k == 3:                                 # truncated
+            m = m[:rng.randrange(1, len(m))]
+        elif k == 4 and len(c.votes) > 1:            # a repeated voter
+            v = c.votes[0]
+            c.votes[1] = v
+            m = bytearray(W.message(c))
+        elif k == 5:                                 # worker id the author does not have
+            h.payload = {_rb(rng, 32): 7}
+            h.id = h.digest()
+            h.sig = orc.sign(sk[author], author, h.id)
+            c2 = W.Certificate(h, c.votes)
+            m = bytearray(W.message(c2))
+        wires.append(bytes(m))
+    return keys, wires
+
+
+@pytest.mark.gpu
+def test_core_device_ingest_many_chunks(monkeypatch):
+    """nt_certificates_ingest over 1,200 certificates of a 10-key committee in
+    chunks of 128 messages (several chunks in flight on two streams), with a
+    corruption mix: the same DagError per message as the host SoA path."""
+    from _oracle import load
+    orc = load()
+    rng = random.Random(5150)
+    nk, quorum = 10, 7
+    keys, wires = _cert_batch(orc, rng, nk, 1200, quorum)
+    monkeypatch.setenv("NT_INGEST_CHUNK", "128")
+    core = N.Core(np.frombuffer(b"".join(keys), np.uint8), [1] * nk, [2] * nk, 9, None, True)
+    try:
+        a, _ = core.ingest(*N.pack(wires), threads=4)
+        c, host = core.ingest(*N.pack(wires), threads=4, device=True)
+        diff = [(i, N.DAG_ERRORS[x], N.DAG_ERRORS[y]) for i, (x, y) in enumerate(zip(a, c)) if x != y]
+        assert not diff, diff[:10]
+        assert host < len(wires) // 3  # the bulk is decided on the device
+        counts = {N.DAG_ERRORS[x]: int((a == x).sum()) for x in set(a.tolist())}
+        assert counts.get("Ok", 0) > 500 and counts.get("InvalidSignature", 0) > 100, counts
+        assert len(counts) >= 5, counts
     finally:
         core.close()
