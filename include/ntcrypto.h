@@ -197,6 +197,18 @@ int nt_certificates_ingest(nt_ctx *ctx, const nt_committee *cm, const uint8_t *d
 int nt_set_small_call_path(nt_ctx *ctx, int mode, int threads);
 /* Host entry-point calls served on host threads / on the GPU so far. */
 int nt_call_counts(const nt_ctx *ctx, uint64_t *host_calls, uint64_t *gpu_calls);
+/* The cost model AUTO routes by.  The first nt_set_small_call_path that enables
+ * the path calibrates it on this context: the host lane's verify_strict time
+ * and SHA-512 rate on one thread, the pool wake-up on `threads` threads, and
+ * the GPU floors from real calls (a one-signature verify, a 64-byte and a
+ * 1 MiB digest); NT_SMALL_* environment variables override single fields.
+ * out9 = cpu_verify_us, gpu_verify_us, cpu_sha_mbs, gpu_lane_mbs, gpu_call_us,
+ * pcie_gbs, spawn_us, threads, calibrated (0/1).  A verify call of n signatures
+ * runs on the host iff ceil(n / T) * cpu_verify_us + (T > 1 ? spawn_us : 0) <
+ * gpu_verify_us (T = min(threads, n)); a digest call iff max(longest, total /
+ * T) / cpu_sha_mbs + (T > 1 ? spawn_us : 0) < gpu_call_us + longest /
+ * gpu_lane_mbs + total / (1000 pcie_gbs) (bytes, microseconds). */
+int nt_small_call_model(const nt_ctx *ctx, double *out9);
 
 /* ---- pinned host buffers ---------------------------------------------
  * Page-locked host memory for callers that stage large batches themselves

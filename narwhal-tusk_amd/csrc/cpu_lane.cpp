@@ -153,16 +153,33 @@ class Pool {
   bool stop_ = false;
 };
 
-Pool& pool(int threads) {
-  static Pool p(std::max(1, std::min(64, threads) - 1));
+// One pool per process, sized once for the machine (at most 64 threads with
+// the caller): a call's parallelism is its item count, capped by the pool.
+int machine_threads() {
+  const unsigned hw = std::thread::hardware_concurrency();
+  return std::max(1, std::min(64, (int)(hw ? hw : 1)));
+}
+Pool& pool() {
+  static Pool p(machine_threads() - 1);
   return p;
 }
 
 }  // namespace
 
 void parallel_for_fn(uint64_t n, int threads, const std::function<void(uint64_t)>& fn) {
-  pool(threads).run(n, fn);
+  // at most `threads` threads work on this call: it becomes T contiguous ranges
+  const uint64_t T = std::min<uint64_t>(n, (uint64_t)std::max(1, std::min(threads, machine_threads())));
+  if (T == n) {
+    pool().run(n, fn);
+    return;
+  }
+  const std::function<void(uint64_t)> range = [&](uint64_t t) {
+    for (uint64_t i = n * t / T; i < n * (t + 1) / T; ++i) fn(i);
+  };
+  pool().run(T, range);
 }
+
+int pool_threads() { return machine_threads(); }
 
 void init(int threads) {
   std::call_once(g_once, [threads] { build(threads); });

@@ -36,6 +36,10 @@ void sha512_trunc32(const uint8_t* msg, uint64_t len, uint8_t out32[32]);
 // verify_batch under SURVEY A.3).  Requires init().
 bool verify(int mode, const uint8_t pk32[32], const uint8_t sig64[64], const uint8_t* msg, uint64_t len);
 
+// threads the worker pool runs with the caller (min(64, hardware threads)): the
+// most parallelism a host-lane call gets
+int pool_threads();
+
 // fn(i) for i in [0, n) on the lane's persistent worker pool plus the calling
 // thread (threads <= 1 or n <= 1: inline).  Safe to call from several threads
 // at once: each call is a job the pool's workers share with its caller.

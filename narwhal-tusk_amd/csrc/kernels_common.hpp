@@ -87,6 +87,9 @@ struct WsATab {
       base[q * kQuadStride] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
   }
   NT_D NT_INLINE void load(uint32_t entry, ge_cached& c) const {
+#ifdef NT_EXPERIMENT_CACHED_ATAB
+    entry = entry >= kTabR ? kTabR + 1 : 1;  // timing experiment only (wrong results): lookups hit one entry
+#endif
     uint32_t w[40];
     const uint4* base = at(entry);
 #pragma unroll

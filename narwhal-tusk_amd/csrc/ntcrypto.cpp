@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
@@ -44,6 +45,22 @@ bool is_pinned(const void* p, uint64_t bytes) {
 
 using namespace ntrt;
 
+static double env_or(const char* name, double dflt) {
+  const char* e = std::getenv(name);
+  return e && *e ? std::atof(e) : dflt;
+}
+static NtSmallModel with_env(NtSmallModel m) {
+  m.cpu_verify_us = env_or("NT_SMALL_CPU_VERIFY_US", m.cpu_verify_us);
+  m.gpu_verify_us = env_or("NT_SMALL_GPU_VERIFY_US", m.gpu_verify_us);
+  m.cpu_sha_mbs = env_or("NT_SMALL_CPU_SHA_MBS", m.cpu_sha_mbs);
+  m.gpu_lane_mbs = env_or("NT_SMALL_GPU_LANE_MBS", m.gpu_lane_mbs);
+  m.gpu_call_us = env_or("NT_SMALL_GPU_CALL_US", m.gpu_call_us);
+  m.pcie_gbs = env_or("NT_SMALL_PCIE_GBS", m.pcie_gbs);
+  m.spawn_us = env_or("NT_SMALL_SPAWN_US", m.spawn_us);
+  return m;
+}
+static int calibrate_small(nt_ctx* ctx);
+
 extern "C" {
 
 const char* nt_strerror(int code) {
@@ -68,6 +85,7 @@ static int init_common(nt_ctx** out, const std::vector<int>& ords) {
   if (!out) return NT_EINVAL;
   *out = nullptr;
   auto ctx = std::make_unique<nt_ctx>();
+  ctx->small_model = with_env(NtSmallModel{});
   const int slots = std::max(1, std::min(8, (int)env_slots()));
   for (int o : ords) {
     auto d = std::make_unique<Device>();
@@ -120,9 +138,26 @@ int nt_num_devices(const nt_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; 
 int nt_set_small_call_path(nt_ctx* ctx, int mode, int threads) {
   if (!ctx || mode < NT_SMALL_OFF || mode > NT_SMALL_ALWAYS) return NT_EINVAL;
   if (threads <= 0) threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  threads = std::min(threads, nt::cpu::pool_threads());  // the host lane's real parallelism
+  ctx->small_mode = NT_SMALL_OFF;  // calibration runs the GPU paths
   ctx->small_threads = threads;
-  if (mode != NT_SMALL_OFF) nt::cpu::init(threads);
+  if (mode != NT_SMALL_OFF) {
+    nt::cpu::init(threads);
+    if (!ctx->small_model.calibrated) {
+      const int rc = calibrate_small(ctx);
+      if (rc != NT_OK) return rc;
+    }
+  }
   ctx->small_mode = mode;
+  return NT_OK;
+}
+
+int nt_small_call_model(const nt_ctx* ctx, double* out9) {
+  if (!ctx || !out9) return NT_EINVAL;
+  const NtSmallModel& m = ctx->small_model;
+  const double v[9] = {m.cpu_verify_us, m.gpu_verify_us, m.cpu_sha_mbs, m.gpu_lane_mbs, m.gpu_call_us,
+                       m.pcie_gbs,      m.spawn_us,      (double)ctx->small_threads.load(), (double)m.calibrated};
+  std::memcpy(out9, v, sizeof v);
   return NT_OK;
 }
 
@@ -349,33 +384,14 @@ Device* dev_of(nt_ctx* ctx, int dev) {
 }
 
 // ---- small-call path (cpu_lane.hpp) -----------------------------
-// Cost model of one host entry-point call, from the `latency` block of
-// bench.py on MI355X + EPYC 9575F (profiles/r02/bench_latency_v1.json: host lane
-// 31-35 us per verify and 884 MB/s of SHA-512 per thread; a GPU verify call
-// below one round 1.33 ms, a lone 508,052-B digest 16.9 ms).  A GPU call below one
-// round of resident waves costs a fixed floor (launch + copies + the two
-// signatures every lane of the verify kernel runs); the digest kernel's time
-// is set by its LONGEST message (one lane's serial chain) plus the PCIe copy.
-// NT_SMALL_* environment variables override the constants (A/B runs).
-double env_or(const char* name, double dflt) {
-  const char* e = std::getenv(name);
-  return e && *e ? std::atof(e) : dflt;
-}
-struct SmallModel {
-  double cpu_verify_us, gpu_verify_us, cpu_sha_mbs, gpu_lane_mbs, gpu_call_us, pcie_gbs, spawn_us;
-  SmallModel()
-      : cpu_verify_us(env_or("NT_SMALL_CPU_VERIFY_US", 36.0)),
-        gpu_verify_us(env_or("NT_SMALL_GPU_VERIFY_US", 1300.0)),
-        cpu_sha_mbs(env_or("NT_SMALL_CPU_SHA_MBS", 850.0)),
-        gpu_lane_mbs(env_or("NT_SMALL_GPU_LANE_MBS", 30.0)),
-        gpu_call_us(env_or("NT_SMALL_GPU_CALL_US", 60.0)),
-        pcie_gbs(env_or("NT_SMALL_PCIE_GBS", 20.0)),
-        spawn_us(env_or("NT_SMALL_SPAWN_US", 15.0)) {}
-};
-const SmallModel& small_model() {
-  static const SmallModel m;
-  return m;
-}
+// Cost model of one host entry-point call (NtSmallModel, runtime.hpp).  A GPU
+// call below one round of resident waves costs a fixed floor (launch + copies
+// + the two signatures every lane of the verify kernel runs); the digest
+// kernel's time is set by its LONGEST message (one lane's serial chain) plus
+// the PCIe copy.  nt_set_small_call_path calibrates the fields on the
+// context's host threads and device (calibrate_small below); NT_SMALL_*
+// environment variables override single fields (A/B runs).
+const NtSmallModel& small_model(const nt_ctx* ctx) { return ctx->small_model; }
 
 int small_threads(const nt_ctx* ctx, uint64_t items) {
   const uint64_t t = (uint64_t)std::max(1, ctx->small_threads.load());
@@ -387,7 +403,7 @@ bool small_verify(nt_ctx* ctx, uint64_t nsig) {
   const int mode = ctx->small_mode.load();
   if (mode == NT_SMALL_ALWAYS) return true;
   if (mode != NT_SMALL_AUTO || !nt::cpu::ready()) return false;
-  const SmallModel& m = small_model();
+  const NtSmallModel& m = small_model(ctx);
   const int T = small_threads(ctx, nsig);
   const double cpu = std::ceil((double)nsig / T) * m.cpu_verify_us + (T > 1 ? m.spawn_us : 0.0);
   return cpu < m.gpu_verify_us;
@@ -397,7 +413,7 @@ bool small_sha(nt_ctx* ctx, uint64_t n, const uint64_t* len) {
   const int mode = ctx->small_mode.load();
   if (mode == NT_SMALL_ALWAYS) return true;
   if (mode != NT_SMALL_AUTO) return false;
-  const SmallModel& m = small_model();
+  const NtSmallModel& m = small_model(ctx);
   uint64_t total = 0, mx = 0;
   for (uint64_t i = 0; i < n; ++i) {
     total += len[i];
@@ -1005,3 +1021,98 @@ int nt_dev_ed25519_sign(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_see
 }
 
 }  // extern "C"
+
+// ---- calibration of the small-call cost model (nt_set_small_call_path) ------
+// Host lane: verify_strict of the RFC 8032 section 7.1 TEST 1 vector (a valid
+// signature over the empty message) and SHA-512 of 1 MiB, on the calling
+// thread; the pool wake-up from a no-op call on `threads` threads.  GPU: one
+// signature through nt_ed25519_verify_strict (below one round: the launch +
+// copy floor), a 64-byte digest (the digest call floor) and a 1 MiB digest
+// (one lane's serial chain), medians of a few calls after a warm-up.
+// NT_SMALL_* variables override single fields afterwards.
+static double median_of(std::vector<double> v) {
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+static int calibrate_small(nt_ctx* ctx) {
+  using clk = std::chrono::steady_clock;
+  auto us = [](clk::time_point a) { return std::chrono::duration<double, std::micro>(clk::now() - a).count(); };
+  static const uint8_t kPk[32] = {0xd7, 0x5a, 0x98, 0x01, 0x82, 0xb1, 0x0a, 0xb7, 0xd5, 0x4b, 0xfe,
+                                  0xd3, 0xc9, 0x64, 0x07, 0x3a, 0x0e, 0xe1, 0x72, 0xf3, 0xda, 0xa6,
+                                  0x23, 0x25, 0xaf, 0x02, 0x1a, 0x68, 0xf7, 0x07, 0x51, 0x1a};
+  static const uint8_t kSig[64] = {0xe5, 0x56, 0x43, 0x00, 0xc3, 0x60, 0xac, 0x72, 0x90, 0x86, 0xe2, 0xcc, 0x80,
+                                   0x6e, 0x82, 0x8a, 0x84, 0x87, 0x7f, 0x1e, 0xb8, 0xe5, 0xd9, 0x74, 0xd8, 0x73,
+                                   0xe0, 0x65, 0x22, 0x49, 0x01, 0x55, 0x5f, 0xb8, 0x82, 0x15, 0x90, 0xa3, 0x3b,
+                                   0xac, 0xc6, 0x1e, 0x39, 0x70, 0x1c, 0xf9, 0xb4, 0x6b, 0xd2, 0x5b, 0xf5, 0xf0,
+                                   0x59, 0x5b, 0xbe, 0x24, 0x65, 0x51, 0x41, 0x43, 0x8e, 0x7a, 0x10, 0x0b};
+  static const uint8_t kEmpty[1] = {0};
+  NtSmallModel m;
+  // host lane, one thread
+  bool ok = nt::cpu::verify(nt::kStrict, kPk, kSig, kEmpty, 0);
+  {
+    std::vector<double> t;
+    for (int r = 0; r < 5; ++r) {
+      const auto a = clk::now();
+      for (int k = 0; k < 8; ++k) ok &= nt::cpu::verify(nt::kStrict, kPk, kSig, kEmpty, 0);
+      t.push_back(us(a) / 8);
+    }
+    if (!ok) return NT_EHIP;  // the host lane must accept a known-good signature
+    m.cpu_verify_us = median_of(t);
+  }
+  std::vector<uint8_t> big(1u << 20, 0x5a);
+  {
+    uint8_t d[32];
+    std::vector<double> t;
+    for (int r = 0; r < 3; ++r) {
+      const auto a = clk::now();
+      nt::cpu::sha512_trunc32(big.data(), big.size(), d);
+      t.push_back(us(a));
+    }
+    m.cpu_sha_mbs = (double)big.size() / median_of(t);  // bytes per us = MB/s
+  }
+  {
+    const int T = std::max(1, ctx->small_threads.load());
+    std::vector<double> t;
+    for (int r = 0; r < 7; ++r) {
+      const auto a = clk::now();
+      nt::cpu::parallel_for((uint64_t)T, T, [](uint64_t) {});
+      t.push_back(us(a));
+    }
+    m.spawn_us = T > 1 ? median_of(t) : 0.0;
+  }
+  // GPU floors (the caller set small_mode = OFF: these calls run the kernels)
+  {
+    const uint64_t off = 0, len = 0;
+    uint8_t bm = 0;
+    std::vector<double> t;
+    for (int r = 0; r < 6; ++r) {
+      const auto a = clk::now();
+      NT_CHK0(nt_ed25519_verify_strict(ctx, kPk, kSig, kEmpty, &off, &len, 1, &bm));
+      if (r) t.push_back(us(a));
+    }
+    if (!(bm & 1)) return NT_EHIP;
+    m.gpu_verify_us = median_of(t);
+  }
+  {
+    uint8_t d[32];
+    const uint64_t off = 0, len64 = 64, len1m = big.size();
+    std::vector<double> ts, tb;
+    for (int r = 0; r < 6; ++r) {
+      auto a = clk::now();
+      NT_CHK0(nt_sha512_trunc32(ctx, big.data(), &off, &len64, 1, d));
+      if (r) ts.push_back(us(a));
+    }
+    for (int r = 0; r < 3; ++r) {
+      auto a = clk::now();
+      NT_CHK0(nt_sha512_trunc32(ctx, big.data(), &off, &len1m, 1, d));
+      if (r) tb.push_back(us(a));
+    }
+    m.gpu_call_us = median_of(ts);
+    const double lane = median_of(tb) - m.gpu_call_us - (double)big.size() / (m.pcie_gbs * 1e3);
+    m.gpu_lane_mbs = (double)big.size() / std::max(lane, 1.0);
+  }
+  m.calibrated = 1;
+  ctx->small_model = with_env(m);
+  return NT_OK;
+}

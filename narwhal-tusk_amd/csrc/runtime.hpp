@@ -324,8 +324,24 @@ struct Device {
 
 }  // namespace ntrt
 
+// Cost model of the small-call path (ntcrypto.cpp: small_verify / small_sha):
+// host-lane and GPU-call costs, calibrated by nt_set_small_call_path on the
+// context's own host threads and device (NT_SMALL_* environment variables
+// override single fields for A/B runs).  The defaults are round-2 measurements.
+struct NtSmallModel {
+  double cpu_verify_us = 36.0;   // one host-lane verify_strict on one thread
+  double gpu_verify_us = 1300.0; // a GPU verify call below one round of resident waves
+  double cpu_sha_mbs = 850.0;    // host-lane SHA-512, one thread
+  double gpu_lane_mbs = 30.0;    // one GPU lane's serial SHA-512 chain
+  double gpu_call_us = 60.0;     // a GPU digest call's fixed cost (launch + copies)
+  double pcie_gbs = 20.0;        // host -> device copy of digest inputs
+  double spawn_us = 15.0;        // waking the host lane's worker pool
+  int calibrated = 0;
+};
+
 struct nt_ctx {
   std::vector<std::unique_ptr<ntrt::Device>> devs;
+  NtSmallModel small_model;  // written by nt_set_small_call_path before small_mode
   // small-call path (cpu_lane.hpp): NT_SMALL_OFF / AUTO / ALWAYS, host threads
   std::atomic<int> small_mode{NT_SMALL_OFF};
   std::atomic<int> small_threads{1};

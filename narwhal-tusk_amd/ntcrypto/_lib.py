@@ -33,7 +33,7 @@ EXPORTED = [
     "nt_dev_ed25519_verify", "nt_dev_group_and", "nt_dev_ed25519_sign", "nt_keyset_create",
     "nt_keyset_free", "nt_keyset_flags", "nt_keyset_info", "nt_ed25519_verify_keyset", "nt_ed25519_verify_batch_groups_keyset",
     "nt_dev_ed25519_verify_keyset", "nt_host_alloc", "nt_host_free", "nt_set_small_call_path", "nt_call_counts",
-    "nt_committee_create", "nt_committee_free", "nt_certificates_ingest",
+    "nt_committee_create", "nt_committee_free", "nt_certificates_ingest", "nt_small_call_model",
 ]
 
 
@@ -87,6 +87,7 @@ def load_library(path=None):
                                                  _vp, _u64, _vp]
     lib.nt_set_small_call_path.argtypes = [_vp, ctypes.c_int, ctypes.c_int]
     lib.nt_call_counts.argtypes = [_vp, _u64p, _u64p]
+    lib.nt_small_call_model.argtypes = [_vp, ctypes.POINTER(ctypes.c_double)]
     _lib = lib
     return lib
 
@@ -159,6 +160,17 @@ class Backend:
         import weakref
         weakref.finalize(buf, self.lib.nt_host_free, ctypes.c_void_p(p))
         return arr
+
+    def small_call_model(self):
+        """The small-call cost model AUTO routes by (nt_small_call_model)."""
+        out = (ctypes.c_double * 9)()
+        _check(self.lib.nt_small_call_model(self.ctx, out), "nt_small_call_model")
+        keys = ("cpu_verify_us", "gpu_verify_us", "cpu_sha_mbs", "gpu_lane_mbs", "gpu_call_us", "pcie_gbs",
+                "spawn_us", "threads", "calibrated")
+        d = dict(zip(keys, list(out)))
+        d["threads"] = int(d["threads"])
+        d["calibrated"] = bool(d["calibrated"])
+        return d
 
     def call_counts(self):
         """(host-lane calls, GPU calls) of the host entry points so far."""

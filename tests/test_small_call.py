@@ -178,3 +178,63 @@ def test_c_abi_auto_small_on_host_large_on_gpu(be, oracle):
         assert (h4 - h3, g4 - g3) == (1, 0)
     finally:
         be.set_small_call_path(ntcrypto.NT_SMALL_OFF)
+
+
+@pytest.mark.gpu
+def test_c_abi_auto_follows_calibrated_model(be):
+    """The first AUTO nt_set_small_call_path calibrates the cost model on this
+    context (host-lane verify / SHA-512 on one thread, pool wake-up, GPU call
+    floors from real calls); AUTO routing then follows it: a verify call of the
+    model's crossover size n* runs on the host lane and n* + 1 on the GPU, and
+    the same for a digest call of 4 KiB messages."""
+    import math
+
+    import ntcrypto
+    T = 4
+    be.set_small_call_path(ntcrypto.NT_SMALL_AUTO, T)
+    try:
+        m = be.small_call_model()
+        assert m["calibrated"] and m["threads"] == T
+        assert 5 < m["cpu_verify_us"] < 500 and 100 < m["gpu_verify_us"] < 20000, m
+        assert 50 < m["cpu_sha_mbs"] < 5000 and m["gpu_lane_mbs"] > 1 and m["gpu_call_us"] > 1, m
+
+        def host_verify(n):
+            t = min(T, n)
+            return math.ceil(n / t) * m["cpu_verify_us"] + (m["spawn_us"] if t > 1 else 0.0) < m["gpu_verify_us"]
+
+        def host_sha(n, L):
+            t = min(T, n)
+            cpu = max(L, n * L / t) / m["cpu_sha_mbs"] + (m["spawn_us"] if t > 1 else 0.0)
+            gpu = m["gpu_call_us"] + L / m["gpu_lane_mbs"] + n * L / (m["pcie_gbs"] * 1e3)
+            return cpu < gpu
+
+        def crossover(pred, limit):
+            ns = [n for n in range(1, limit) if pred(n)]
+            return max(ns) if ns and max(ns) < limit - 1 else None
+
+        rng = np.random.default_rng(17)
+        nv = crossover(host_verify, 4000)
+        assert nv is not None, m
+        n = nv + 1
+        seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        msg = rng.integers(0, 256, n * 32, dtype=np.uint8)
+        off = np.arange(n, dtype=np.uint64) * 32
+        ln = np.full(n, 32, np.uint64)
+        pk, sig = be.sign_batch(seeds, msg, off, ln)
+        for k, where in ((nv, "host"), (nv + 1, "gpu")):
+            h0, g0 = be.call_counts()
+            assert be.verify_strict(pk[:k], sig[:k], msg, off[:k], ln[:k]).all()
+            h1, g1 = be.call_counts()
+            assert (h1 - h0, g1 - g0) == ((1, 0) if where == "host" else (0, 1)), (k, where, m)
+        L = 4096
+        ns = crossover(lambda k: host_sha(k, L), 20000)
+        if ns is not None:
+            blob = rng.integers(0, 256, (ns + 1) * L, dtype=np.uint8)
+            for k, where in ((ns, "host"), (ns + 1, "gpu")):
+                msgs = [blob[i * L:(i + 1) * L].tobytes() for i in range(k)]
+                h0, g0 = be.call_counts()
+                be.digest_many(msgs)
+                h1, g1 = be.call_counts()
+                assert (h1 - h0, g1 - g0) == ((1, 0) if where == "host" else (0, 1)), (k, where, m)
+    finally:
+        be.set_small_call_path(ntcrypto.NT_SMALL_OFF)
