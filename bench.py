@@ -182,6 +182,9 @@ def main():
     dev = torch.device("cuda", local)
 
     import ntcrypto
+    # precondition (INTEGRATION.md "PyTorch in the same process"): torch's bundled
+    # HIP runtime starts before libntcrypto maps its tables
+    assert torch.cuda.is_initialized(), "torch's HIP runtime must be initialised before nt_init"
     be = ntcrypto.Backend(device=local)
     # a real (non-null) stream: the library launches on it and the HIP events
     # bracketing the timed region are recorded on it
@@ -452,27 +455,37 @@ def bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_r
            "valu_issue_share": round(pv["valu_issue_share_4cyc"], 3) if "valu_issue_share_4cyc" in pv else None,
            "note": "k_sha512_pipe: per 64 messages a producer wave expands K+W into LDS, a consumer wave runs the rounds; bound by the consumer wave's serial per-block stream (latency-bound, SURVEY H2), not HBM; valu_issue_share from the PMC profile (256 consumer + 256 producer waves on 1,024 SIMDs)",
            "spot_check_ok": bool(ok)}
-    # the shard one GPU holds when the driver runs config 4 on 8 GPUs
-    # (16,384 / 8 = 2,048 messages = 32 consumer waves): its per-GPU rate
-    m8 = (m_total + 7) // 8
-    if world == 1 and m >= m8 > 0:
-        def step8():
-            be.dev_sha512(0, sp, data.data_ptr(), off.data_ptr(), ln.data_ptr(), m8, out.data_ptr())
-        step8()
-        barrier()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(steps):
-            step8()
-        e1.record(stream)
-        barrier()
-        k8 = e0.elapsed_time(e1) / steps
-        res["shard_of_8"] = {"messages": m8, "kernel_ms": round(k8, 3),
-                             "gb_per_s_per_gpu": round(m8 * ml / (k8 * 1e-3) / 1e9, 2),
-                             "note": "one GPU's share of config 4 at 8 GPUs: the same serial per-message chain "
-                                     "(~3,907 blocks), 8x fewer messages, so the per-GPU rate is 1/8 and the "
-                                     "8-GPU aggregate stays at the 1-GPU figure"}
+    # the shards one GPU holds when config 4 runs on N = 2 / 4 / 8 GPUs: each is
+    # timed on this GPU, and the N-GPU aggregate follows as N x its per-GPU rate.
+    # A lane per message is bound by one lane's serial ~3,907-block chain, so the
+    # shard takes about as long as the whole batch: the aggregate stays flat.
+    if world == 1 and m:
+        res["shard_of"] = {}
+        res["expected_aggregate_gbs"] = {"1": res["value"]}
+        for N in (2, 4, 8):
+            mN = (m_total + N - 1) // N
+            if mN > m:
+                continue
+
+            def stepN():
+                be.dev_sha512(0, sp, data.data_ptr(), off.data_ptr(), ln.data_ptr(), mN, out.data_ptr())
+            stepN()
+            barrier()
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(steps):
+                stepN()
+            e1.record(stream)
+            barrier()
+            kN = e0.elapsed_time(e1) / steps
+            per = mN * ml / (kN * 1e-3) / 1e9
+            res["shard_of"][str(N)] = {"messages": mN, "kernel_ms": round(kN, 3), "gb_per_s_per_gpu": round(per, 2)}
+            res["expected_aggregate_gbs"][str(N)] = round(N * per, 2)
+        res["scaling_note"] = ("config 4 does not scale with GPUs: a message's SHA-512 is one serial Merkle-Damgard "
+                               "chain (~3,907 blocks of 500,000 B), so a GPU's shard of 16,384 / N messages takes "
+                               "about as long as the whole batch; expected_aggregate_gbs = N x the measured per-GPU "
+                               "rate of that shard on this GPU")
     # the same shard through the host entry point from pinned host memory
     # (PCIe-inclusive: BASELINE.md reports GPU numbers with and without H2D)
     if m:
@@ -828,9 +841,10 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
             "workload": "cfg3: %d certificates, committee n=%d, %d votes + 1 header signature each, "
                         "%d-byte header preimage" % (G_total, nk, quorum, hlen),
             "scaling": "strong (certificates sharded over ranks)",
-            "pipelining": "keyset: consecutive steps (independent 100k-certificate batches) on two streams, each "
-                          "with its own digest / verdict buffers (the device API alternates its two key-cache "
-                          "stashes); keyset_one_stream: the same launches strictly back to back on one stream",
+            "pipelining": "keyset: consecutive steps re-verify the SAME 100k certificates (resident inputs), "
+                          "alternating two streams, each with its own digest / verdict buffers (the device API "
+                          "alternates its two key-cache stashes), every buffer's verdicts checked; "
+                          "keyset_one_stream: the same launches strictly back to back on one stream",
             "key_cache": {"comb_bits": ks_bits, "gb_per_device": round(ks_bytes / 1e9, 2),
                           "build_s": round(ks_build_s, 3),
                           "note": "per-key wide combs of -A (13 comb additions per [k]A at 20 bits; [s]B: 11 "
@@ -985,6 +999,18 @@ def bench_latency(be, pk_h, sig_h, msg_h, L):
                    "auto = NT_SMALL_AUTO (calls below the crossover on host threads)"}
     for mode, name in ((ntcrypto.NT_SMALL_OFF, "gpu"), (ntcrypto.NT_SMALL_AUTO, "auto")):
         be.set_small_call_path(mode, 0)
+        if mode == ntcrypto.NT_SMALL_AUTO:
+            # the cost model AUTO routes by, calibrated on this context by the call above
+            m = be.small_call_model()
+            T = m["threads"]
+            nv = 0
+            while nv < 100000:
+                t = min(T, nv + 1)
+                if -(-(nv + 1) // t) * m["cpu_verify_us"] + (m["spawn_us"] if t > 1 else 0) >= m["gpu_verify_us"]:
+                    break
+                nv += 1
+            out["small_call_model"] = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in m.items()}
+            out["small_call_model"]["verify_crossover_signatures"] = nv
         for case, (fn, reps) in cases.items():
             h0, g0 = be.call_counts()
             fn()

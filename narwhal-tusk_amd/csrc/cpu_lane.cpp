@@ -54,6 +54,10 @@ struct HostATab {
   ge_cached e[18];
   void store(uint32_t j, const ge_cached& c) { e[j] = c; }
   void load(uint32_t j, ge_cached& c) const { c = e[j]; }
+  void load_signed(uint32_t e0, int32_t d, ge_cached& c) const {
+    c = e[e0 + (uint32_t)(d < 0 ? -d : d)];
+    ge_cached_cneg(c, d < 0);
+  }
 };
 
 void build(int threads) {

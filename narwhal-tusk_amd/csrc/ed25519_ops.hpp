@@ -1,7 +1,8 @@
 // ed25519_ops.hpp -- per-lane Ed25519 operations shared by the gfx950 kernels
 // (k_*.hip) and the host-compiled harness (tests/cpp/nt_host_harness.cpp,
 // tools/opcount.py).  Table storage is abstracted:
-//   ATab:  store(entry, ge_cached) / load(entry, ge_cached&)    j*(-A), j = 0..8, per lane
+//   ATab:  store(entry, ge_cached) / load_signed(e0, d, ge_cached&)   j*(-A), j = 0..8, per lane
+//          (load_signed: entry e0 + |d|, negated when d < 0)
 //   WComb: load(pos, idx, ge_niels&)                            idx * 2^(16 pos) * P (wide comb)
 //
 // Semantics (restated from ed25519-dalek 1.0.1 /
@@ -235,6 +236,9 @@ NT_HD NT_INLINE void wcomb_fill(uint32_t* dst, uint32_t* tmp, const uint32_t* ba
 constexpr uint32_t kTabR = 9;  // first entry of the R table
 
 // store j * (neg ? -P : P), j = 0..8, at entries e0 .. e0+8
+#ifndef NT_TAB_DBL
+#define NT_TAB_DBL 0
+#endif
 template <class ATab>
 NT_HD NT_INLINE void ptab_build(const ge_p3& P, uint32_t neg, ATab& at, uint32_t e0) {
   ge_p3 Q;
@@ -254,6 +258,38 @@ NT_HD NT_INLINE void ptab_build(const ge_p3& P, uint32_t neg, ATab& at, uint32_t
   at.store(e0, c0);
   ge_p3_to_cached(c1, Q);
   at.store(e0 + 1, c1);
+#if NT_TAB_DBL
+  // 2Q, 4Q, 8Q by doubling (4S + 4M each instead of an 8M addition); right after
+  // each, its odd neighbour from the point still in registers: 3Q = 2Q + Q,
+  // 5Q = 4Q + Q, 7Q = 8Q - Q, and finally 6Q = 7Q - Q (no table reloads:
+  // a store followed by a load of the same entry is a full memory round trip)
+  {
+    ge_cached cn = c1;
+    ge_cached_cneg(cn, 1u);  // -Q
+    ge_p3 cur = Q, nb;
+#pragma unroll 1
+    for (uint32_t j = 2; j <= 8; j <<= 1) {
+      ge_p2 q;
+      ge_p3_to_p2(q, cur);
+      ge_cp t;
+      ge_dbl(t, q);
+      ge_cp_to_p3(cur, t);
+      ge_cached c;
+      ge_p3_to_cached(c, cur);
+      at.store(e0 + j, c);
+      ge_add_cached(t, cur, j == 8 ? cn : c1);
+      ge_cp_to_p3(nb, t);
+      ge_p3_to_cached(c, nb);
+      at.store(e0 + (j == 8 ? 7u : j + 1u), c);
+    }
+    ge_cp t;
+    ge_add_cached(t, nb, cn);  // 7Q - Q
+    ge_cp_to_p3(nb, t);
+    ge_cached c;
+    ge_p3_to_cached(c, nb);
+    at.store(e0 + 6, c);
+  }
+#else
   ge_p3 cur = Q;
 #pragma unroll 1
   for (uint32_t j = 2; j < 9; ++j) {
@@ -264,6 +300,7 @@ NT_HD NT_INLINE void ptab_build(const ge_p3& P, uint32_t neg, ATab& at, uint32_t
     ge_p3_to_cached(cj, cur);
     at.store(e0 + j, cj);
   }
+#endif
 }
 
 // wave-uniform maximum: every lane of a wave then runs the same window count
@@ -286,13 +323,13 @@ NT_HD NT_INLINE int32_t w4_digit(const uint32_t d[8], int wi) {
 }
 
 // acc (completed -> p3) + table entry e0 + |d| with the sign of d
+// (ATab::load_signed: the entry of |d|, negated when d < 0)
 template <class ATab>
 NT_HD NT_INLINE void ladder_add(ge_cp& t, int32_t d, uint32_t e0, const ATab& at) {
   ge_cached ce;
-  at.load(e0 + (uint32_t)(d < 0 ? -d : d), ce);  // latency overlaps the conversion
+  at.load_signed(e0, d, ce);  // latency overlaps the conversion
   ge_p3 u;
   ge_cp_to_p3(u, t);
-  ge_cached_cneg(ce, d < 0);
   ge_add_cached(t, u, ce);
 }
 
@@ -303,10 +340,10 @@ NT_HD NT_INLINE void ladder_ar(ge_cp& t, const uint32_t ud[8], const uint32_t vd
   {
     const int32_t d = w4_digit(ud, W - 1);
     ge_cached ce;
-    at.load((uint32_t)(d < 0 ? -d : d), ce);
-    ge_cached_cneg(ce, d < 0);
+    at.load_signed(0, d, ce);
     // cached (Y+X, Y-X, 2Z, .) -> (2X : 2Y : 2Z) as a completed point with T = Z
-    fe_sub(t.X, ce.YpX, ce.YmX);
+    // (cached sums are not carried: subtract with 4p)
+    fe_sub4(t.X, ce.YpX, ce.YmX);
     fe_carry(t.X);
     fe_add(t.Y, ce.YpX, ce.YmX);
     fe_carry(t.Y);

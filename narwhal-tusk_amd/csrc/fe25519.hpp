@@ -91,6 +91,13 @@ NT_HD NT_INLINE void fe_sub4(fe& h, const fe& f, const fe& g) {
   for (int i = 1; i < 10; ++i) h.v[i] = f.v[i] + ((i & 1) ? 0x7fffffcu : 0xffffffcu) - g.v[i];
 }
 
+// h = 2f + 4p - g   (f reduced, g as fe_sub4): one shift-add and one subtract per limb
+NT_HD NT_INLINE void fe_dbl_sub4(fe& h, const fe& f, const fe& g) {
+  h.v[0] = (f.v[0] << 1) + (0xfffffb4u - g.v[0]);
+#pragma unroll
+  for (int i = 1; i < 10; ++i) h.v[i] = (f.v[i] << 1) + (((i & 1) ? 0x7fffffcu : 0xffffffcu) - g.v[i]);
+}
+
 // h = 2p - f  (f reduced)
 NT_HD NT_INLINE void fe_neg(fe& h, const fe& f) {
   h.v[0] = 0x7ffffdau - f.v[0];

@@ -46,32 +46,49 @@ NT_HD NT_INLINE void ge_cp_to_p3(ge_p3& r, const ge_cp& p) {
 }
 NT_HD NT_INLINE void ge_p3_to_p2(ge_p2& r, const ge_p3& p) { r.X = p.X; r.Y = p.Y; r.Z = p.Z; }
 
+// Cached entries are only ever g operands of fe_mul (ge_add_cached) or swapped /
+// negated (ge_cached_cneg: T2d is a multiply output), so their sums need no carry:
+// from "R" coordinates Y + X < 2^27 (even) / 2^26.01 (odd), Y + 2p - X < 2^27.58,
+// 2Z < 2^27 -- all within fe_mul's g bound 2^27.75.  (The ladder's seed, which
+// subtracts two of them, uses fe_sub4.)
+#ifndef NT_CACHED_NOCARRY
+#define NT_CACHED_NOCARRY 0
+#endif
 NT_HD NT_INLINE void ge_p3_to_cached(ge_cached& r, const ge_p3& p) {
   fe d2;
   fe_const(d2, kFeD2);
   fe_add(r.YpX, p.Y, p.X);
-  fe_carry(r.YpX);
   fe_sub(r.YmX, p.Y, p.X);
-  fe_carry(r.YmX);
   fe_add(r.Z2, p.Z, p.Z);
+#if !NT_CACHED_NOCARRY
+  fe_carry(r.YpX);
+  fe_carry(r.YmX);
   fe_carry(r.Z2);
+#endif
   fe_mul(r.T2d, p.T, d2);
 }
 
 // 2P from a p2 point with "R" coordinates (dalek ProjectivePoint::double).
 NT_HD NT_INLINE void ge_dbl(ge_cp& r, const ge_p2& p) {
-  fe XX, YY, ZZ2, S, t;
+  fe XX, YY, ZZ, S, t;
   fe_sq(XX, p.X);
   fe_sq(YY, p.Y);
-  fe_sq(ZZ2, p.Z);
-  fe_add(ZZ2, ZZ2, ZZ2);      // < 2^27
+  fe_sq(ZZ, p.Z);
   fe_add(t, p.X, p.Y);        // < 2^27 (sq_wide input bound)
   fe_sq_wide(S, t);
   fe_add(r.Y, YY, XX);        // Y' = YY + XX           < 2^27
   fe_sub(r.Z, YY, XX);        // Z' = YY - XX (2p)      < 2^27.6
   fe_sub4(r.X, S, r.Y);       // X' = S - Y'  (4p)      < 2^28.6 -> carry
   fe_carry(r.X);
-  fe_sub4(r.T, ZZ2, r.Z);     // T' = 2ZZ - Z' (4p)     < 2^28.6 (f-side only)
+#ifndef NT_DBL_SUB4
+#define NT_DBL_SUB4 0
+#endif
+#if NT_DBL_SUB4
+  fe_dbl_sub4(r.T, ZZ, r.Z);  // T' = 2ZZ - Z' (4p)     < 2^28.6 (f-side only)
+#else
+  fe_add(ZZ, ZZ, ZZ);
+  fe_sub4(r.T, ZZ, r.Z);
+#endif
 }
 
 // P + Q (neg=0) or P - Q (neg=1), Q cached with "R" coordinates.

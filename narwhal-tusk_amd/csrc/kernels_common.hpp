@@ -18,7 +18,14 @@ constexpr int kBlock = 256;
 // signatures per lane per block iteration of k_ed25519_verify (1 or 2; A/B builds)
 constexpr int kVPer = NT_VERIFY_PER_LANE;
 constexpr int kAEntries = 18;         // j*(+-A) and j*(-R), |digit| in 0..8
-constexpr int kAQuads = 10;           // uint4 per cached entry (40 words)
+// Signed entries (NT_ATAB_SIGNED=1): each cached coordinate in its own 3-quad
+// slot -- Y+X, Y-X, 2Z, 2dT and -2dT -- so a lookup of digit -j reads the slots
+// of +j in swapped order (per-lane addresses) instead of negating the entry
+// with 10 subtracts and 30 selects (ge_cached_cneg) on every ladder addition.
+#ifndef NT_ATAB_SIGNED
+#define NT_ATAB_SIGNED 0
+#endif
+constexpr int kAQuads = NT_ATAB_SIGNED ? 15 : 10;  // uint4 per entry
 
 // --------------------------------------------------------------------------
 // Table accessors
@@ -75,6 +82,48 @@ struct WsATab {
     return ws + ((size_t)(slot * kAEntries + entry) * kAQuads) * kBlock + threadIdx.x;
   }
 #endif
+#if NT_ATAB_SIGNED
+  // slot k of an entry: 3 quads, words 0..9 used
+  NT_D NT_INLINE void store_fe(uint4* q, const fe& f) const {
+    q[0 * kQuadStride] = make_uint4(f.v[0], f.v[1], f.v[2], f.v[3]);
+    q[1 * kQuadStride] = make_uint4(f.v[4], f.v[5], f.v[6], f.v[7]);
+    q[2 * kQuadStride] = make_uint4(f.v[8], f.v[9], 0u, 0u);
+  }
+  NT_D NT_INLINE void load_fe(const uint4* q, fe& f) const {
+    const uint4 a = q[0 * kQuadStride], b = q[1 * kQuadStride], c = q[2 * kQuadStride];
+    f.v[0] = a.x; f.v[1] = a.y; f.v[2] = a.z; f.v[3] = a.w;
+    f.v[4] = b.x; f.v[5] = b.y; f.v[6] = b.z; f.v[7] = b.w;
+    f.v[8] = c.x; f.v[9] = c.y;
+  }
+  NT_D NT_INLINE void store(uint32_t entry, const ge_cached& c) const {
+    uint4* base = at(entry);
+    fe n;
+    fe_neg(n, c.T2d);  // T2d is a multiply output (reduced): 2p - T2d < 2^27
+    store_fe(base, c.YpX);
+    store_fe(base + 3 * kQuadStride, c.YmX);
+    store_fe(base + 6 * kQuadStride, c.Z2);
+    store_fe(base + 9 * kQuadStride, c.T2d);
+    store_fe(base + 12 * kQuadStride, n);
+  }
+  // entry e0 + |d| negated when d < 0: -(Y+X, Y-X, 2Z, 2dT) = (Y-X, Y+X, 2Z, -2dT)
+  NT_D NT_INLINE void load_signed(uint32_t e0, int32_t d, ge_cached& c) const {
+    const uint32_t neg = d < 0 ? 1u : 0u;
+    uint32_t entry = e0 + (uint32_t)(d < 0 ? -d : d);
+#ifdef NT_EXPERIMENT_CACHED_ATAB
+    entry = entry >= kTabR ? kTabR + 1 : 1;  // timing experiment only (wrong results): lookups hit one entry
+#endif
+    const uint4* base = at(entry);
+    load_fe(base + (neg ? 3 : 0) * kQuadStride, c.YpX);
+    load_fe(base + (neg ? 0 : 3) * kQuadStride, c.YmX);
+    load_fe(base + 6 * kQuadStride, c.Z2);
+    load_fe(base + (neg ? 12 : 9) * kQuadStride, c.T2d);
+  }
+  NT_D NT_INLINE void load(uint32_t entry, ge_cached& c) const { load_signed(entry, 0, c); }
+#else
+  NT_D NT_INLINE void load_signed(uint32_t e0, int32_t d, ge_cached& c) const {
+    load(e0 + (uint32_t)(d < 0 ? -d : d), c);
+    ge_cached_cneg(c, d < 0);
+  }
   NT_D NT_INLINE void store(uint32_t entry, const ge_cached& c) const {
     uint32_t w[40];
 #pragma unroll
@@ -102,6 +151,7 @@ struct WsATab {
       c.YpX.v[i] = w[i]; c.YmX.v[i] = w[10 + i]; c.Z2.v[i] = w[20 + i]; c.T2d.v[i] = w[30 + i];
     }
   }
+#endif
 };
 
 // ---- key-cache verification: up to 8 signatures per lane, one inversion -----

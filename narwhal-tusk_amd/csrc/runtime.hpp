@@ -388,15 +388,21 @@ inline std::vector<std::pair<uint64_t, uint64_t>> shard(uint64_t n, size_t ndev,
   return r;
 }
 
-// A free execution slot of device entry d, locked into lk.  Latency-sized
-// calls try the extra (high-priority) slots first, bulk calls the entry's own
-// slot first; when every slot is busy, wait for the preferred one.
+// The execution slot of device entry d a call runs on, locked into lk.  Bulk
+// calls take the entry's own slot (waiting for it), so the extra
+// high-priority slots stay free for latency-sized calls; a latency-sized call
+// takes the first free extra slot, else the entry's own slot if free, else
+// waits for the first extra slot (two concurrent bulk calls must
+// not occupy both slots and block a certificate-sized call behind a digest).
 inline Device& acquire_slot(nt_ctx* ctx, size_t d, bool latency, std::unique_lock<std::mutex>& lk) {
   Device& p = *ctx->devs[d];
+  if (!latency || p.extra.empty()) {
+    lk = std::unique_lock<std::mutex>(p.mu);
+    return p;
+  }
   std::vector<Device*> order;
-  if (!latency) order.push_back(&p);
   for (auto& x : p.extra) order.push_back(x.get());
-  if (latency) order.push_back(&p);
+  order.push_back(&p);
   for (Device* s : order) {
     std::unique_lock<std::mutex> l(s->mu, std::try_to_lock);
     if (l.owns_lock()) {

@@ -87,7 +87,8 @@ def load_library(path=None):
                                                  _vp, _u64, _vp]
     lib.nt_set_small_call_path.argtypes = [_vp, ctypes.c_int, ctypes.c_int]
     lib.nt_call_counts.argtypes = [_vp, _u64p, _u64p]
-    lib.nt_small_call_model.argtypes = [_vp, ctypes.POINTER(ctypes.c_double)]
+    if hasattr(lib, "nt_small_call_model"):  # absent from older A/B builds (NTCRYPTO_LIB)
+        lib.nt_small_call_model.argtypes = [_vp, ctypes.POINTER(ctypes.c_double)]
     _lib = lib
     return lib
 
@@ -110,11 +111,23 @@ def _unpack(bm, n):
     return np.unpackbits(bm, bitorder="little")[:n].astype(bool)
 
 
+def _torch_first():
+    """PyTorch-ROCm wheels bundle their own HIP runtime.  Two runtimes in one
+    process work when torch's starts first; torch's first HIP init AFTER
+    libntcrypto has mapped its tables fails ("PyTorch in the
+    same process").  If this process has imported torch, start its runtime now."""
+    import sys
+    torch = sys.modules.get("torch")
+    if torch is not None and torch.cuda.is_available() and not torch.cuda.is_initialized():
+        torch.cuda.init()
+
+
 class Backend:
     """A context over one or more gfx950 devices (nt_init / nt_init_device)."""
 
     def __init__(self, num_gpus=0, device=None, devices=None):
         self.lib = load_library()
+        _torch_first()
         ctx = _vp()
         if devices is not None:
             arr = (ctypes.c_int * len(devices))(*devices)

@@ -31,6 +31,7 @@ def pytest_collection_finish(session):
         return
     if torch.cuda.is_available():
         torch.cuda.init()
+        assert torch.cuda.is_initialized(), "torch's HIP runtime must start before libntcrypto's nt_init"
 
 
 @pytest.fixture(scope="session")
