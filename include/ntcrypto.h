@@ -74,9 +74,10 @@ int nt_init_device(nt_ctx **out, int device_ordinal);
 /* An explicit list of device ordinals; repeats are allowed (each entry gets
  * its own stream, tables and workspace), which lets the multi-device sharding
  * of the host entry points be exercised on a single GPU.
- * Device memory per entry: the wide comb of B (24-bit digits, 11.8 GB; 872 MB
- * in a -DNT_BCOMB_BITS=20 build) + the verify workspace (~1.5 GB at 2,048 slots)
- * + grow-only staging -- so a repeated ordinal pays it once per repeat. */
+ * Device memory: the wide comb of B (24-bit digits, 11.8 GB; 872 MB in a
+ * -DNT_BCOMB_BITS=20 build) once per device ordinal per process, shared by
+ * every entry and context on that ordinal; per entry the verify workspace
+ * (~1.5 GB at 2,048 slots) + grow-only staging. */
 int nt_init_devices(nt_ctx **out, const int *ordinals, int n);
 void nt_free(nt_ctx *ctx);
 int nt_num_devices(const nt_ctx *ctx);

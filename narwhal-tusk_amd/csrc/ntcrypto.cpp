@@ -41,6 +41,28 @@ bool is_pinned(const void* p, uint64_t bytes) {
   return (uintptr_t)p + bytes <= it->first + it->second;
 }
 
+// comb of B per device ordinal, shared across device entries and contexts
+std::mutex g_combb_mu;
+std::map<int, std::weak_ptr<CombB>> g_combb;
+
+std::shared_ptr<CombB> shared_comb_b(Device& dv, int& rc) {
+  static const uint32_t kB[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                                 0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};  // encoding of B
+  std::lock_guard<std::mutex> lk(g_combb_mu);
+  if (auto c = g_combb[dv.ordinal].lock()) return c;
+  auto c = std::make_shared<CombB>();
+  c->ordinal = dv.ordinal;
+  if (hipMalloc(&c->p, nt::wcomb_bytes_per_key(nt::bcomb_bits())) != hipSuccess) {
+    c->p = nullptr;
+    rc = NT_ENOMEM;
+    return nullptr;
+  }
+  rc = dv.build_wcombs(nt::bcomb_bits(), kB, 1, 0, c->p, nullptr);
+  if (rc != NT_OK) return nullptr;
+  g_combb[dv.ordinal] = c;
+  return c;
+}
+
 }  // namespace ntrt
 
 using namespace ntrt;

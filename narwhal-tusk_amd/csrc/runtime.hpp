@@ -76,10 +76,27 @@ bool is_pinned(const void* p, uint64_t bytes);
 
 enum { B_DATA, B_OFF, B_LEN, B_PK, B_SIG, B_OUT, B_OUT2, B_FIRST, B_CNT, B_STASH, B_SORT, B_NBUF };
 
+// The wide comb of B on one device ordinal, shared by every device entry of
+// every context of the process that runs on that ordinal (11.8 GB at 24-bit
+// digits: round 2 paid it per entry -- repeated ordinals, a second Backend, the
+// contention probe's contexts).  Built by the first user, freed
+// with the last (ntcrypto.cpp: shared_comb_b).
+struct CombB {
+  int ordinal = -1;
+  uint32_t* p = nullptr;
+  ~CombB() {
+    if (!p) return;
+    (void)hipSetDevice(ordinal);
+    (void)hipFree(p);
+  }
+};
+struct Device;
+std::shared_ptr<CombB> shared_comb_b(Device& dv, int& rc);
+
 struct Device {
   int ordinal = -1;
   int group = -1;               // index of this device entry in nt_ctx::devs (keyset tables)
-  bool owns_comb = true;        // false for the extra slots (they share the entry's comb of B)
+  std::shared_ptr<CombB> combB;  // holds d_combB (shared per ordinal, see CombB)
   hipStream_t stream = nullptr;
   uint32_t* d_combB = nullptr;  // wide comb of B (verify, key-cache verify, sign)
   void* d_ws = nullptr;
@@ -123,7 +140,6 @@ struct Device {
       if (b.p) (void)hipHostFree(b.p);
     extra.clear();  // before this entry's comb, which the extra slots borrow
     (void)hipSetDevice(ordinal);
-    if (d_combB && owns_comb) (void)hipFree(d_combB);
     if (d_ws) (void)hipFree(d_ws);
     if (ws_done) (void)hipEventDestroy(ws_done);
     if (stash_done) (void)hipEventDestroy(stash_done);
@@ -170,13 +186,13 @@ struct Device {
     NT_TRY(hipEventCreateWithFlags(&ws2_done, hipEventDisableTiming));
     NT_TRY(hipEventCreateWithFlags(&stash2_done, hipEventDisableTiming));
     if (share) {
+      combB = share->combB;
       d_combB = share->d_combB;
-      owns_comb = false;
     } else {
-      static const uint32_t kB[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
-                                     0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
-      if (hipMalloc(&d_combB, nt::wcomb_bytes_per_key(nt::bcomb_bits())) != hipSuccess) return NT_ENOMEM;
-      NT_CHK0(build_wcombs(nt::bcomb_bits(), kB, 1, 0, d_combB, nullptr));
+      int rc = NT_OK;
+      combB = shared_comb_b(*this, rc);
+      if (!combB) return rc;
+      d_combB = combB->p;
     }
     // Workspace slots = grid cap of the verify kernel.  Four times the resident
     // workgroups (256-thread blocks, `occupancy` waves per SIMD, 4 SIMDs per CU):
