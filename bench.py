@@ -325,6 +325,12 @@ def main():
                 "mads_per_verify": mads,
                 "valu_instr_per_verify": round(pvl["SQ_INSTS_VALU"] * 64 / PMC_N) if "SQ_INSTS_VALU" in pvl else None,
                 "valu_issue_share": round(pv["valu_issue_share_4cyc"], 3) if "valu_issue_share_4cyc" in pv else None,
+                "effective_clock_ghz": round(pv["effective_clock_ghz"], 3) if "effective_clock_ghz" in pv else None,
+                "frac_at_effective_clock": (round(achieved / (MAD_PEAK_TS * pv["effective_clock_ghz"] / 2.4), 4)
+                                            if "effective_clock_ghz" in pv else None),
+                "clock_note": "effective clock of the config-2 launch in the PMC profile: GRBM_GUI_ACTIVE / 8 / the "
+                              "dispatch's duration (MI355X_MICROARCH.md, DVFS give-back); frac_at_effective_clock "
+                              "prices the mad peak at that clock instead of 2.4 GHz",
                 "issue_note": "the kernel is VALU-issue-bound (issue share from the PMC profile); non-mad VALU work "
                               "(carries, pre-scaling, SHA-512, lattice reduction) is why mad frac < issue share"}
 
@@ -827,6 +833,14 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                     "streams": slots(cached), "mismatches_vs_expected": mism}
         if key == "keyset" and fused and kev:
             out[key]["roofline"] = keyset_roofline(np.mean([a.elapsed_time(b) for a, b in kev]), kms, V + G)
+        if key == "keyset_one_stream" and kev and "keyset" in out and out["keyset"].get("roofline"):
+            # launches strictly back to back: each one's own duration (sort + key-cache kernel +
+            # byte pack, what rocprof sums per step) without the two-stream overlap
+            own = float(np.mean([a.elapsed_time(b) for a, b in kev]))
+            rf = out["keyset"]["roofline"]
+            ach = rf["mads_per_signature"] * (V + G) / (own * 1e-3) / 1e12
+            rf["launch_ms_one_stream"] = round(own, 3)
+            rf["frac_one_stream_launch"] = round(ach / MAD_PEAK_TS, 4)
     if world == 1 and fused and os.environ.get("NT_BENCH_SHARDS", "1") != "0":
         out["shard_of"] = bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, stream, barrier, G, quorum,
                                             dict(hdr_flat=hdr_flat, h_off=h_off, h_len=h_len, cpre=cpre, c_off=c_off,
@@ -964,8 +978,9 @@ def keyset_roofline(launch_ms, step_ms, nsig):
             "achieved": round(achieved, 3), "peak": round(MAD_PEAK_TS, 2), "unit": "Tmad/s",
             "frac": round(achieved / MAD_PEAK_TS, 4),
             "frac_vs_measured_mad_rate": round(achieved / MAD_MEASURED_TS, 4),
-            "valu_instr_per_signature": (round(pkl["SQ_INSTS_VALU"] * 64 / (grid * 8)) if grid and "SQ_INSTS_VALU" in pkl
-                                         else None),
+            # the profile's launch is the same 6.9M-signature config-3 launch (NT_BENCH_SHARDS=0 in the PMC pass)
+            "valu_instr_per_signature": (round(pkl["SQ_INSTS_VALU"] * 64 / nsig) if "SQ_INSTS_VALU" in pkl else None),
+            "effective_clock_ghz": round(pk["effective_clock_ghz"], 3) if "effective_clock_ghz" in pk else None,
             "valu_issue_share": round(pk["valu_issue_share_4cyc"], 3) if "valu_issue_share_4cyc" in pk else None,
             "traffic": pk.get("hbm_bytes_per_launch"),
             "traffic_note": "HBM bytes per launch (profiles/%s, FETCH_SIZE*2 + WRITE_SIZE): 24 random 128-B comb "

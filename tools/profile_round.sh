@@ -5,7 +5,7 @@
 #   3. PMC passes for the cfg3 key-cache launch
 # Usage: bash tools/profile_round.sh <tag>
 set -euo pipefail
-TAG=${1:-r02c}
+TAG=${1:-r03}
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -13,6 +13,6 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run -- pyt
 echo "stats done"
 PMC_BENCH_ARGS="--no-certs --no-ingest --no-latency" bash tools/pmc_collect.sh "$OUT/pmc"
 python3 tools/pmc_summarize.py "$OUT/pmc" "$OUT/pmc_verify_sha.json" "cfg2 verify + cfg4 SHA-512" > /dev/null
-PMC_BENCH_ARGS="--no-sha --no-ingest --no-latency --sigs 65536" bash tools/pmc_collect.sh "$OUT/pmc_keyset"
+NT_BENCH_SHARDS=0 PMC_BENCH_ARGS="--no-sha --no-ingest --no-latency --sigs 65536" bash tools/pmc_collect.sh "$OUT/pmc_keyset"
 python3 tools/pmc_summarize.py "$OUT/pmc_keyset" "$OUT/pmc_keyset.json" "cfg3 key-cache launch" > /dev/null
 echo "pmc done"
