@@ -237,7 +237,7 @@ constexpr uint32_t kTabR = 9;  // first entry of the R table
 
 // store j * (neg ? -P : P), j = 0..8, at entries e0 .. e0+8
 #ifndef NT_TAB_DBL
-#define NT_TAB_DBL 0
+#define NT_TAB_DBL 1
 #endif
 template <class ATab>
 NT_HD NT_INLINE void ptab_build(const ge_p3& P, uint32_t neg, ATab& at, uint32_t e0) {

@@ -52,7 +52,7 @@ NT_HD NT_INLINE void ge_p3_to_p2(ge_p2& r, const ge_p3& p) { r.X = p.X; r.Y = p.
 // 2Z < 2^27 -- all within fe_mul's g bound 2^27.75.  (The ladder's seed, which
 // subtracts two of them, uses fe_sub4.)
 #ifndef NT_CACHED_NOCARRY
-#define NT_CACHED_NOCARRY 0
+#define NT_CACHED_NOCARRY 1
 #endif
 NT_HD NT_INLINE void ge_p3_to_cached(ge_cached& r, const ge_p3& p) {
   fe d2;
