@@ -47,8 +47,8 @@ METRIC = "Ed25519 verifies/sec + SHA-512 GB/s at 1/2/4/8 MI355X vs dalek host-co
 MAD_PEAK_TS = 256 * 4 * 64 * 2.4e9 / 4 / 1e12  # v_mad_u64_u32: 4 cycles per wave64 per SIMD
 MAD_MEASURED_TS = 32.80  # profiles/r01_alu_rate.txt (tools/microbench): 4.80 cycles per wave64 per SIMD
 HBM_PEAK_GBS = 8000.0
-PMC_PROFILE = os.path.join("r02", "pmc_verify_sha.json")  # tools/profile_round.sh + tools/pmc_summarize.py
-PMC_KEYSET_PROFILE = os.path.join("r02", "pmc_keyset.json")  # cfg3 key-cache launch, 8 signatures per lane
+PMC_PROFILE = os.path.join("r03", "pmc_verify_sha.json")  # tools/profile_round.sh + tools/pmc_summarize.py
+PMC_KEYSET_PROFILE = os.path.join("r03", "pmc_keyset.json")  # cfg3 key-cache launch, 8 signatures per lane
 PMC_N = 1_000_000  # signatures per launch in that profile (the default config-2 run)
 SODIUM = "/opt/conda/lib/libsodium.so.23"
 
@@ -317,9 +317,10 @@ def main():
                 "traffic_note": ("HBM bytes per launch from rocprofv3 FETCH_SIZE*2 + WRITE_SIZE (profiles/%s, "
                                  "same kernel build, separate --pmc passes; the config-2 launch, grouped by grid size). "
                                  "Algorithmic minimum ~2.0 KB/verify (608 B of input + 11 comb lines of B); the rest "
-                                 "(~13.4 KB/verify of the ~21.9 KB measured, plus line over-fetch) is this kernel's own "
-                                 "per-lane [j]A/[j]R table workspace (2,880 B written, ~10.5 KB read), ~11x the "
-                                 "minimum in all -- 2.1 TB/s, not the limiter of an issue-bound kernel" % PMC_PROFILE)
+                                 "(%.1f KB/verify measured) is this kernel's own per-lane [j]A/[j]R table workspace "
+                                 "(2,880 B written, ~10.5 KB read) plus line over-fetch -- ~2.1 TB/s, not the limiter "
+                                 "of an issue-bound kernel"
+                                 % (PMC_PROFILE, (pv.get("hbm_bytes_per_launch") or 0) / PMC_N / 1e3))
                 if pv else None,
                 "kernel": "k_ed25519_verify<strict>", "kernel_ms": round(kernel_ms, 3),
                 "mads_per_verify": mads,

@@ -518,13 +518,13 @@ NT_HD NT_INLINE uint32_t compare_one(const ge_p2& P, const fe& zi, const uint32_
 //   ld.get(j, meta, Aw, Rw, Sw, msg, len, ca)   inputs of signature j
 //   st.put(j, P, prefix) / st.get_point(j, P) /  per-lane stash of R'_j and the
 //   st.get_prefix(j, prefix)                     running product Z_0 .. Z_j
-// Returns bit j = verdict of signature j.  The stash keeps the registers of a
+// Returns bit j = verdict of signature j (m <= 64).  The stash keeps the registers of a
 // lane independent of N (the kernel's stash lives in global memory); m <= N
 // signatures are run (the kernel's run-time per-lane count).
 template <int MODE, int N, class Loader, class WCombB, class Stash>
-NT_HD NT_INLINE uint32_t verify_cached_batch(const Loader& ld, const WCombB& cb, Stash& st, int m = N) {
-  static_assert(N >= 1 && N <= 32, "verdict bits of a lane are one word");
-  uint32_t okbits = 0, strictbits = 0;
+NT_HD NT_INLINE uint64_t verify_cached_batch(const Loader& ld, const WCombB& cb, Stash& st, int m = N) {
+  static_assert(N >= 1 && N <= 64, "verdict bits of a lane are one 64-bit word");
+  uint64_t okbits = 0, strictbits = 0;
   fe acc;
 #pragma unroll 1
   for (int j = 0; j < m; ++j) {
@@ -534,8 +534,8 @@ NT_HD NT_INLINE uint32_t verify_cached_batch(const Loader& ld, const WCombB& cb,
     typename Loader::Comb ca;
     ld.get(j, meta, Aw, Rw, Sw, msg, len, ca);
     ge_p3 P;
-    okbits |= cached_point<MODE>(P, meta, Aw, Rw, Sw, msg, len, ca, cb) << j;
-    strictbits |= (is_strict<MODE>(meta) ? 1u : 0u) << j;
+    okbits |= (uint64_t)cached_point<MODE>(P, meta, Aw, Rw, Sw, msg, len, ca, cb) << j;
+    strictbits |= (uint64_t)(is_strict<MODE>(meta) ? 1u : 0u) << j;
     if (j == 0) acc = P.Z;
     else fe_mul(acc, acc, P.Z);
     ge_p2 P2;
@@ -559,7 +559,7 @@ NT_HD NT_INLINE uint32_t verify_cached_batch(const Loader& ld, const WCombB& cb,
     }
     uint32_t Rw[8];
     ld.rbytes(j, Rw);
-    okbits &= ~((compare_one<MODE>(P, zi, Rw, (strictbits >> j) & 1u) ^ 1u) << j);
+    okbits &= ~((uint64_t)(compare_one<MODE>(P, zi, Rw, (strictbits >> j) & 1u) ^ 1u) << j);
   }
   return okbits;
 }

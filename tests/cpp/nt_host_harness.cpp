@@ -301,7 +301,7 @@ int nth_verify_cached_n(int mode, int nsig, const uint8_t* pk, const uint8_t* si
   g_fe_sq = cs;
   HostLoader ld{A, S, msgs, lens, meta, ca};
   HostStash st;
-  uint32_t bits;
+  uint64_t bits;
   if ((mode & 0xff) == kMixed) {  // mode = kMixed | strict_mask << 8 (the kernel's key_idx bit 31)
     for (int j = 0; j < nsig; ++j)
       if ((mode >> (8 + j)) & 1) meta[j] |= kKeyWantStrict;
