@@ -24,6 +24,8 @@
 // next one prefetched during the current addition); [u](+-A) + [v](-R) use
 // joint 4-bit windows over per-lane 9-entry cached tables in a global
 // workspace laid out lane-major, so a lookup's loads use whole lines.
+#include <algorithm>
+
 #include "kernels_common.hpp"
 
 namespace nt {
@@ -603,11 +605,15 @@ uint64_t verify_grid(uint64_t n, uint32_t ws_slots) {
 
 // signatures one wave of resident workgroups covers (every CU full at the
 // kernel's occupancy): launches sized in whole rounds leave no partial last wave
-uint64_t keyset_round_sigs(uint32_t cus) { return (uint64_t)cus * 4 * keyset_occ() * 64 * keyset_per_lane(); }
+// host-side chunk sizing of the pipelined entry points: 8 rows per wave (round 2's
+// grid; the launch plan itself is ks_plan's, whatever the chunk)
+uint64_t keyset_round_sigs(uint32_t cus) {
+  return (uint64_t)cus * 4 * keyset_occ() * 64 * std::min<uint32_t>(keyset_per_lane(), 8);
+}
 uint64_t verify_round_sigs(uint32_t cus) { return (uint64_t)cus * verify_occupancy() * kVPer * kBlock; }
-// most rows (signatures per lane) of a key-cache chunk, one inversion each: 8
-// (the 4 / 6 / 8 / 12 / 16 A/B in DESIGN.md §5.2); NT_KEYSET_PER_LANE in
-// [1, kKsPerLane] caps it for A/B runs
+// most rows (signatures per lane) of a key-cache chunk, one inversion each: 64,
+// the plan picks the chunk size (ks_plan.hpp; round-3 A/B in DESIGN.md §5.2);
+// NT_KEYSET_PER_LANE in [1, kKsPerLane] caps it for A/B runs
 uint32_t keyset_per_lane() {
   static const uint32_t m = (uint32_t)env_occ("NT_KEYSET_PER_LANE", kKsPerLane, 1, kKsPerLane);
   return m;

@@ -154,9 +154,9 @@ struct WsATab {
 #endif
 };
 
-// ---- key-cache verification: up to 8 signatures per lane, one inversion -----
+// ---- key-cache verification: up to 64 signatures per lane, one inversion ----
 #ifndef NT_KS_PER_LANE
-#define NT_KS_PER_LANE 8
+#define NT_KS_PER_LANE 64
 #endif
 // most signatures per lane sharing one inversion; a launch runs
 // keyset_per_lane() <= kKsPerLane of them (a kernel argument)

@@ -7,15 +7,20 @@
 // accumulates per lane (A = 16.66 k: the comb additions, SHA-512, compare;
 // B = 15.07 k: the inversion; profiles/opcount.json).  The plan launches a
 // persistent grid of `waves` waves (2 or 3 per SIMD) and cuts the rows into
-// chunks = k x waves chunks of `base_rows` or `base_rows + 1` rows (k = the
-// fewest rounds with at most `cap` rows per chunk), so every wave runs k
-// chunks of (nearly) equal size: no SIMD ends with a lone tail wave, which
-// the fixed 8-rows-per-wave grid of round 2 left at 4.32, 2.16, 1.08 and 0.54
-// rounds per launch for config 3 on 1, 2, 4 and 8 GPUs.
-// Between 2 and 3 waves per SIMD the plan takes the cheaper of
-//   k (A pmax + B) x (waves per SIMD) / T(waves per SIMD)
-// with T(2) = 0.97, T(3) = 1 (issue rate of 2 vs 3 resident waves, measured
-// on the key-cache kernel: profiles/r01/ab_occ_v9).
+// chunks = k x waves chunks of `base_rows` or `base_rows + 1` rows (at most
+// `cap`), so every wave runs k chunks of (nearly) equal size: no SIMD ends with
+// a lone tail wave, which the fixed 8-rows-per-wave grid of round 2 left at
+// 4.32, 2.16, 1.08 and 0.54 rounds per launch for config 3 on 1, 2, 4 and 8
+// GPUs.  Candidates: 2 or 3 waves per SIMD, and k = the fewest
+// rounds at <= cap rows per chunk or, when that is one round, also two; the
+// plan takes the cheapest of
+//   k (A pmax + B) x (waves per SIMD) / T(waves per SIMD) x (k == 1 ? L : 1)
+// with T(2) = 0.97, T(3) = 1 (issue rate of 2 vs 3 resident waves,
+// profiles/r01/ab_occ_v9) and L = 1.07: with one claim per wave nothing
+// rebalances waves that run at different speeds, and a one-round plan measured
+// ~7 % slower than the model's relative cost predicts (config 3, 2 waves per
+// SIMD: 52 rows in one chunk 11.07 vs 2 x 26 rows 11.71 M certificates/s;
+// profiles/r03/ab_ks_plan2/).
 #pragma once
 #include <stdint.h>
 
@@ -30,10 +35,11 @@ struct KsPlan {
   uint32_t rounds;     // k: chunks per wave
 };
 
-// force_per_simd: 0 = cheaper of 2 and 3, else 2 or 3; cap: most rows per chunk (1..8)
+// force_per_simd: 0 = cheaper of 2 and 3, else 2 or 3; cap: most rows per chunk (1..64)
 inline KsPlan ks_plan(uint64_t n, uint32_t cus, uint32_t cap, int force_per_simd) {
-  const double A = 16.66, B = 15.07;
+  const double A = 16.66, B = 15.07, kLone = 1.07;
   const uint64_t rows = (n + 63) / 64;
+  if (cap == 0) cap = 1;
   KsPlan best{0, 0, 0, 0, 2, 0};
   double best_t = -1.0;
   for (uint32_t w = 2; w <= 3; ++w) {
@@ -41,17 +47,20 @@ inline KsPlan ks_plan(uint64_t n, uint32_t cus, uint32_t cap, int force_per_simd
     const uint64_t slots = (uint64_t)w * 4 * (cus ? cus : 1);
     const uint64_t W = rows < slots ? rows : slots;
     if (W == 0) return KsPlan{0, 0, 0, 0, w, 0};
-    const uint64_t k = (rows + cap * W - 1) / (cap * W);
-    const uint64_t C = k * W < rows ? k * W : rows;  // cap 1: one row per chunk
-    const uint64_t base = rows / C, extra = rows % C;
-    const uint64_t pmax = base + (extra ? 1 : 0);
-    // waves per SIMD actually resident (a launch smaller than the slots fills fewer)
-    const uint64_t per = (W + 4 * (uint64_t)cus - 1) / (4 * (uint64_t)(cus ? cus : 1));
-    const double T = w == 2 ? 0.97 : 1.0;
-    const double t = (double)k * (A * (double)pmax + B) * (double)per / T;
-    if (best_t < 0 || t < best_t - 1e-9) {
-      best_t = t;
-      best = KsPlan{(uint32_t)W, (uint32_t)C, (uint32_t)base, (uint32_t)extra, w, (uint32_t)k};
+    const uint64_t kmin = (rows + cap * W - 1) / (cap * W);
+    for (uint64_t k = kmin; k <= (kmin > 2 ? kmin : 2); ++k) {
+      const uint64_t C = k * W < rows ? k * W : rows;  // cap 1: one row per chunk
+      if (k > kmin && C == rows) break;                 // a second round of empty chunks
+      const uint64_t base = rows / C, extra = rows % C;
+      const uint64_t pmax = base + (extra ? 1 : 0);
+      // waves per SIMD actually resident (a launch smaller than the slots fills fewer)
+      const uint64_t per = (W + 4 * (uint64_t)cus - 1) / (4 * (uint64_t)(cus ? cus : 1));
+      const double T = w == 2 ? 0.97 : 1.0;
+      const double t = (double)k * (A * (double)pmax + B) * (double)per / T * (k == 1 ? kLone : 1.0);
+      if (best_t < 0 || t < best_t - 1e-9) {
+        best_t = t;
+        best = KsPlan{(uint32_t)W, (uint32_t)C, (uint32_t)base, (uint32_t)extra, w, (uint32_t)k};
+      }
     }
   }
   return best;

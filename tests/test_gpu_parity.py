@@ -293,12 +293,12 @@ def test_keyset_committee_random_vs_oracle(be, oracle):
     ks.close()
 
 
-@pytest.mark.timeout(400)
+@pytest.mark.timeout(560)
 def test_keyset_per_lane_counts():
     """The key-cache kernel is a persistent grid claiming chunks of rows
     (ks_plan.hpp: rounds x waves chunks of base or base + 1 rows, at most
     NT_KEYSET_PER_LANE rows, 2 or 3 waves per SIMD by NT_KEYSET_WAVES or the
-    plan's cost model; both read once per process).  Caps 1, 3, 5 and 8 with
+    plan's cost model; both read once per process).  Caps 1, 3, 5, 8, 26 and 64 with
     forced and automatic wave counts -- partial rows, other chunk sizes, several
     rounds per wave, other inversion batch sizes -- give the corpus verdicts in
     input order, in key-grouped order (72k) and at ~1M signatures (subprocesses:
@@ -307,7 +307,7 @@ def test_keyset_per_lane_counts():
     import subprocess
     import sys
     probe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_keyset_per_lane_probe.py")
-    for m, w in ((1, ""), (3, "3"), (5, "2"), (8, "2"), (8, "3")):
+    for m, w in ((1, ""), (3, "3"), (5, "2"), (8, "2"), (8, "3"), (26, "2"), (64, "")):
         env = dict(os.environ, NT_KEYSET_PER_LANE=str(m), NT_KEYSET_COMB_BITS="16")
         env.pop("NT_KEYSET_WAVES", None)
         if w:
