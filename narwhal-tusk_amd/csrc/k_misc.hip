@@ -412,6 +412,18 @@ constexpr uint64_t kKsMaxPerLaunch = 8ull << 20;
 constexpr uint32_t kSortBuckets = 4096;  // committee keys + 1 "unknown" bucket
 constexpr uint64_t kSortMin = 65536;     // smaller launches keep the input order
 constexpr int kSortTile = 16;            // items per thread of k_key_scatter
+// -DNT_SORT_LEGACY=1 (A/B builds): round-2 histogram (one key per loop iteration, 64 per
+// thread, <= 1024 blocks) and packed counters
+#ifndef NT_SORT_LEGACY
+#define NT_SORT_LEGACY 0
+#endif
+constexpr int kHistTile = NT_SORT_LEGACY ? 1 : 16;  // independent key loads in flight per thread of k_key_hist
+// Global bucket counters one 128-B line apart: every block's flush / reservation
+// is one device-scope atomic per bucket, and with the counters packed 32 to a
+// line those atomics serialize per LINE (rocprof r03b: k_key_scatter 66 us at
+// 1,661 blocks, ~1.6 ns per atomic on one of 4 lines; k_key_hist 43 us whatever
+// the size, one dependent load + LDS atomic per loop iteration).
+constexpr uint32_t kCtrStride = NT_SORT_LEGACY ? 1 : 32;
 
 NT_D NT_INLINE uint32_t sort_bucket(uint32_t k, int mixed, uint32_t nkeys) {
   if (mixed) k &= ~kKeyWantStrict;
@@ -423,11 +435,21 @@ __global__ __launch_bounds__(kBlock) void k_key_hist(const uint32_t* __restrict_
   __shared__ uint32_t h[kSortBuckets];
   for (uint32_t b = threadIdx.x; b <= nkeys; b += kBlock) h[b] = 0;
   __syncthreads();
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
-    atomicAdd(&h[sort_bucket(key[i], mixed, nkeys)], 1u);
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock * kHistTile;
+  for (uint64_t t0 = (uint64_t)blockIdx.x * kBlock * kHistTile; t0 < n; t0 += stride) {
+    uint32_t k[kHistTile];
+#pragma unroll
+    for (int r = 0; r < kHistTile; ++r) {  // all loads issued before the first is used
+      const uint64_t i = t0 + (uint64_t)r * kBlock + threadIdx.x;
+      k[r] = i < n ? key[i] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < kHistTile; ++r)
+      if (t0 + (uint64_t)r * kBlock + threadIdx.x < n) atomicAdd(&h[sort_bucket(k[r], mixed, nkeys)], 1u);
+  }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b <= nkeys; b += kBlock)
-    if (h[b]) atomicAdd(&hist[b], h[b]);
+    if (h[b]) atomicAdd(&hist[b * kCtrStride], h[b]);
 }
 
 // exclusive scan of nb <= kSortBuckets counts (one workgroup; ~4k adds)
@@ -436,7 +458,7 @@ __global__ __launch_bounds__(kBlock) void k_key_scan(const uint32_t* __restrict_
   __shared__ uint32_t part[kBlock];
   const uint32_t per = (nb + kBlock - 1) / kBlock, b0 = threadIdx.x * per;
   uint32_t sum = 0;
-  for (uint32_t b = b0; b < b0 + per && b < nb; ++b) sum += hist[b];
+  for (uint32_t b = b0; b < b0 + per && b < nb; ++b) sum += hist[b * kCtrStride];
   part[threadIdx.x] = sum;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -450,8 +472,8 @@ __global__ __launch_bounds__(kBlock) void k_key_scan(const uint32_t* __restrict_
   __syncthreads();
   uint32_t acc = part[threadIdx.x];
   for (uint32_t b = b0; b < b0 + per && b < nb; ++b) {
-    cursor[b] = acc;
-    acc += hist[b];
+    cursor[b * kCtrStride] = acc;
+    acc += hist[b * kCtrStride];
   }
 }
 
@@ -472,7 +494,7 @@ __global__ __launch_bounds__(kBlock) void k_key_scatter(const uint32_t* __restri
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b <= nkeys; b += kBlock)
-    if (cnt[b]) base[b] = atomicAdd(&cursor[b], cnt[b]);
+    if (cnt[b]) base[b] = atomicAdd(&cursor[b * kCtrStride], cnt[b]);
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < kSortTile; ++r) {
@@ -498,16 +520,26 @@ static bool keyset_sort_enabled() {
   return on;
 }
 
-// d_sort layout: [16 words: chunk counter][hist 4096][cursor 4096][perm m][verdict bytes m]
+// d_sort layout: [16 words: row / chunk counter][hist 4096 x 32][cursor 4096 x 32][perm m][verdict bytes m]
 constexpr size_t kSortHdr = 64;
 size_t keyset_sort_bytes(uint64_t n) {
   const uint64_t m = n < kKsMaxPerLaunch ? n : kKsMaxPerLaunch;
-  return kSortHdr + 2 * kSortBuckets * 4 + (size_t)m * 5 + 64;
+  return kSortHdr + 2 * (size_t)kSortBuckets * kCtrStride * 4 + (size_t)m * 5 + 64;
+}
+
+// NT_KEYSET_STREAM=0 selects the chunked plan (ks_plan) instead of streamed rows
+static bool keyset_stream_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NT_KEYSET_STREAM");
+    return !(e && *e == '0');
+  }();
+  return on;
 }
 
 KsPlan keyset_plan(uint64_t n, uint32_t cus) {
   static const int force = env_occ("NT_KEYSET_WAVES", 0, 2, 3);
-  return ks_plan(n, cus, keyset_per_lane(), force);
+  return keyset_stream_enabled() ? ks_stream_plan(n, cus, keyset_per_lane(), force)
+                                 : ks_plan(n, cus, keyset_per_lane(), force);
 }
 
 hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
@@ -518,8 +550,8 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
   if (!d_sort || !d_stash) return hipErrorInvalidValue;
   uint32_t* ctr = (uint32_t*)d_sort;
   uint32_t* hist = ctr + kSortHdr / 4;
-  uint32_t* cursor = hist + kSortBuckets;
-  uint32_t* p = cursor + kSortBuckets;
+  uint32_t* cursor = hist + kSortBuckets * kCtrStride;
+  uint32_t* p = cursor + kSortBuckets * kCtrStride;
   // launches of at most kKsMaxPerLaunch signatures reuse one stash (stream-ordered)
   for (uint64_t lo = 0; lo < n; lo += kKsMaxPerLaunch) {
     const uint64_t m = n - lo < kKsMaxPerLaunch ? n - lo : kKsMaxPerLaunch;
@@ -531,11 +563,12 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
     if (keyset_sort_enabled() && m >= kSortMin && nkeys + 1 <= kSortBuckets) {
       bytes = (uint8_t*)(p + m);
       const int mixed = mode == kMixed;
-      if ((e = hipMemsetAsync(hist, 0, 4ull * (nkeys + 1), s)) != hipSuccess) return e;
-      // ~64 keys per thread: every block flushes its LDS histogram with one global
-      // atomic per bucket, so fewer blocks = less contention on the nkeys + 1 counters
-      const uint64_t hw = (m + (uint64_t)kBlock * 64 - 1) / ((uint64_t)kBlock * 64);
-      const uint32_t hb = (uint32_t)(hw < 1024 ? hw : 1024);
+      if ((e = hipMemsetAsync(hist, 0, 4ull * kCtrStride * (nkeys + 1), s)) != hipSuccess) return e;
+      // one tile of kHistTile keys per thread and at most 512 blocks (each flushes its
+      // LDS histogram with one global atomic per bucket)
+      const uint64_t per = NT_SORT_LEGACY ? 64 : kHistTile, cap = NT_SORT_LEGACY ? 1024 : 512;
+      const uint64_t hw = (m + (uint64_t)kBlock * per - 1) / ((uint64_t)kBlock * per);
+      const uint32_t hb = (uint32_t)(hw < cap ? hw : cap);
       hipLaunchKernelGGL(k_key_hist, dim3(hb), dim3(kBlock), 0, s, d_key_idx + lo, m, mixed, nkeys, hist);
       hipLaunchKernelGGL(k_key_scan, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)hist, nkeys + 1, cursor);
       const uint64_t sb = (m + (uint64_t)kBlock * kSortTile - 1) / ((uint64_t)kBlock * kSortTile);
@@ -618,11 +651,15 @@ uint32_t keyset_per_lane() {
   static const uint32_t m = (uint32_t)env_occ("NT_KEYSET_PER_LANE", kKsPerLane, 1, kKsPerLane);
   return m;
 }
-// stash of one launch (<= kKsMaxPerLaunch signatures): waves x (most rows of a
-// chunk) x 64 lanes x 160 B, and waves x pmax <= rows + waves <= n / 64 + 1 + 12 cus
+// stash of a call's launches (each <= kKsMaxPerLaunch signatures): waves x
+// (stash rows of a wave) x 64 lanes x 160 B, the larger of the first launch's
+// and the last (partial) launch's plan
 size_t keyset_stash_bytes(uint64_t n, uint32_t cus) {
-  const uint64_t m = n < kKsMaxPerLaunch ? n : kKsMaxPerLaunch;
-  return (size_t)(m + 64 + (uint64_t)64 * 12 * cus) * kKsQuads * 16;
+  const uint64_t first = n < kKsMaxPerLaunch ? n : kKsMaxPerLaunch;
+  const uint64_t last = n > kKsMaxPerLaunch && n % kKsMaxPerLaunch ? n % kKsMaxPerLaunch : first;
+  const KsPlan a = keyset_plan(first, cus), b = keyset_plan(last, cus);
+  const uint64_t ra = (uint64_t)a.waves * a.stash_rows(), rb = (uint64_t)b.waves * b.stash_rows();
+  return (size_t)((ra > rb ? ra : rb) + 1) * 64 * kKsQuads * 16;
 }
 size_t ws_bytes_per_slot() { return (size_t)kAEntries * kAQuads * kBlock * 16; }
 

@@ -33,7 +33,38 @@ struct KsPlan {
   uint32_t extra;
   uint32_t per_simd;   // resident waves per SIMD the launch is sized for (2 or 3)
   uint32_t rounds;     // k: chunks per wave
+  // streamed rows (ks_stream_plan): rows claimed one at a time, up to `prow`
+  // rows per inversion (the stash rows of a wave); chunks / base / extra unused
+  uint32_t stream = 0;
+  uint32_t rows = 0;
+  uint32_t prow = 0;
+  // stash rows of one wave either way
+  uint32_t stash_rows() const { return stream ? prow : base_rows + (extra ? 1u : 0u); }
 };
+
+// Streamed rows: a persistent grid of per_simd x 4 x cus waves (fewer when the
+// launch has fewer rows) in which every wave claims ONE row at a time from the
+// launch's counter and inverts once when the rows run out -- so waves that run
+// at different speeds take different row counts (the one-claim plans above lose
+// ~7 % to exactly that), the inversion is shared by all of a wave's rows instead
+// of a chunk's, and at any moment the grid works on ~`waves` consecutive rows of
+// the key-grouped order (a few committee keys' combs instead of all of them).
+// prow = the average rows per wave + 2 (<= cap): a wave that fills its stash
+// inverts and starts another batch.
+inline KsPlan ks_stream_plan(uint64_t n, uint32_t cus, uint32_t cap, int force_per_simd) {
+  const uint64_t rows = (n + 63) / 64;
+  const uint32_t per = force_per_simd ? (uint32_t)force_per_simd : 2u;
+  const uint64_t slots = (uint64_t)per * 4 * (cus ? cus : 1);
+  const uint64_t W = rows < slots ? rows : slots;
+  KsPlan p{(uint32_t)W, 0, 0, 0, per, 1};
+  p.stream = 1;
+  p.rows = (uint32_t)rows;
+  if (W == 0) return p;
+  uint64_t pr = (rows + W - 1) / W + 2;
+  if (cap == 0) cap = 1;
+  p.prow = (uint32_t)(pr < cap ? pr : cap);
+  return p;
+}
 
 // force_per_simd: 0 = cheaper of 2 and 3, else 2 or 3; cap: most rows per chunk (1..64)
 inline KsPlan ks_plan(uint64_t n, uint32_t cus, uint32_t cap, int force_per_simd) {

@@ -377,4 +377,9 @@ void nth_ks_plan(unsigned long long n, uint32_t cus, uint32_t cap, int force, ui
   const KsPlan p = ks_plan(n, cus, cap, force);
   out[0] = p.waves; out[1] = p.chunks; out[2] = p.base_rows; out[3] = p.extra; out[4] = p.per_simd; out[5] = p.rounds;
 }
+// streamed rows (ks_stream_plan): out = waves, rows, prow, per_simd
+void nth_ks_stream_plan(unsigned long long n, uint32_t cus, uint32_t cap, int force, uint32_t* out) {
+  const KsPlan p = ks_stream_plan(n, cus, cap, force);
+  out[0] = p.waves; out[1] = p.rows; out[2] = p.prow; out[3] = p.per_simd;
+}
 }

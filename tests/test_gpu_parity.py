@@ -295,20 +295,24 @@ def test_keyset_committee_random_vs_oracle(be, oracle):
 
 @pytest.mark.timeout(560)
 def test_keyset_per_lane_counts():
-    """The key-cache kernel is a persistent grid claiming chunks of rows
-    (ks_plan.hpp: rounds x waves chunks of base or base + 1 rows, at most
-    NT_KEYSET_PER_LANE rows, 2 or 3 waves per SIMD by NT_KEYSET_WAVES or the
-    plan's cost model; both read once per process).  Caps 1, 3, 5, 8, 26 and 64 with
-    forced and automatic wave counts -- partial rows, other chunk sizes, several
-    rounds per wave, other inversion batch sizes -- give the corpus verdicts in
-    input order, in key-grouped order (72k) and at ~1M signatures (subprocesses:
-    the variables are read at first use)."""
+    """The key-cache kernel is a persistent grid.  Streamed rows (the default,
+    ks_stream_plan: one row per claim, one inversion per NT_KEYSET_PER_LANE
+    rows at most, a new batch when a wave's stash is full) and the chunked plan
+    (NT_KEYSET_STREAM=0, ks_plan: rounds x waves chunks of base or base + 1
+    rows), at 2 or 3 waves per SIMD by NT_KEYSET_WAVES or the plan (all read
+    once per process).  Caps 1, 3, 5, 8, 26 and 64 with forced and automatic
+    wave counts -- partial rows, several batches per wave, other inversion
+    batch sizes -- give the corpus verdicts in input order, in key-grouped order
+    (72k) and at ~1M signatures (subprocesses: the variables are read at first
+    use)."""
     import json
     import subprocess
     import sys
     probe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_keyset_per_lane_probe.py")
-    for m, w in ((1, ""), (3, "3"), (5, "2"), (8, "2"), (8, "3"), (26, "2"), (64, "")):
-        env = dict(os.environ, NT_KEYSET_PER_LANE=str(m), NT_KEYSET_COMB_BITS="16")
+    cases = [("1", 1, ""), ("1", 3, "3"), ("1", 8, "2"), ("1", 64, ""), ("1", 64, "3"),
+             ("0", 1, ""), ("0", 5, "2"), ("0", 8, "3"), ("0", 26, "2"), ("0", 64, "")]
+    for stream, m, w in cases:
+        env = dict(os.environ, NT_KEYSET_PER_LANE=str(m), NT_KEYSET_COMB_BITS="16", NT_KEYSET_STREAM=stream)
         env.pop("NT_KEYSET_WAVES", None)
         if w:
             env["NT_KEYSET_WAVES"] = w

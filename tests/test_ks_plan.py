@@ -74,3 +74,40 @@ def test_default_cap_plans():
     for n, (w, k, base) in want.items():
         p = check(n, 256, 64, 0)
         assert (p["per_simd"], p["rounds"], p["base"]) == (w, k, base), (n, p)
+
+
+def stream_plan(n, cus=256, cap=64, force=0):
+    out = (ctypes.c_uint32 * 4)()
+    _hostarith.load().nth_ks_stream_plan(ctypes.c_ulonglong(n), cus, cap, force, out)
+    return dict(zip(("waves", "rows", "prow", "per_simd"), list(out)))
+
+
+@pytest.mark.parametrize("cus", [1, 4, 80, 256, 304])
+def test_stream_plan_invariants(cus):
+    """Streamed rows (ks_stream_plan, the default): every SIMD slot of the
+    grid has a wave while rows last, a wave stages at most `cap` rows per
+    inversion and room for two rows above the average, so the stash
+    (waves x prow rows) covers every row of the launch whenever cap allows."""
+    for n in [1, 63, 64, 65, 4095, 65536, 200_000, 850_000, 1_000_000, 1_703_375, 3_406_750, 6_813_500, 8 << 20]:
+        for cap in (1, 3, 8, 26, 64):
+            for force in (0, 2, 3):
+                p = stream_plan(n, cus, cap, force)
+                rows = (n + 63) // 64
+                per = force or 2
+                assert p["per_simd"] == per
+                assert p["rows"] == rows
+                assert p["waves"] == min(rows, per * 4 * cus)
+                avg = math.ceil(rows / p["waves"])
+                assert p["prow"] == min(cap, avg + 2) >= 1
+                if cap >= avg + 2:
+                    assert p["waves"] * p["prow"] >= rows + 2 * p["waves"]
+
+
+def test_stream_plan_config3_shards():
+    """Config 3 (100k certificates x 68 signatures) and its 2/4/8-GPU shards:
+    2 waves per SIMD, one inversion per wave (the stash holds every row a wave
+    takes, with two rows to spare)."""
+    for certs in (100_000, 50_000, 25_000, 12_500):
+        p = stream_plan(certs * 68)
+        assert p["waves"] == 2048
+        assert p["prow"] == math.ceil(p["rows"] / 2048) + 2 <= 64
