@@ -14,6 +14,7 @@
 //   sign_one                  = Keypair::generate + sign   (crypto/src/lib.rs:163-191)
 #pragma once
 #include "fe25519.hpp"
+#include "fe_inv_vt.hpp"
 #include "ge25519.hpp"
 #include "sc25519.hpp"
 #include "sha512.hpp"
@@ -514,6 +515,20 @@ NT_HD NT_INLINE uint32_t compare_one(const ge_p2& P, const fe& zi, const uint32_
   return r;
 }
 
+// The inversion of a key-cache batch (verification is public data): the
+// variable-time binary GCD (fe_inv_vt.hpp) unless -DNT_INV_VT=0 (the Fermat
+// chain, 254 squarings + 11 multiplies).
+#ifndef NT_INV_VT
+#define NT_INV_VT 1
+#endif
+NT_HD NT_INLINE void fe_invert_batch(fe& out, const fe& z) {
+#if NT_INV_VT
+  fe_invert_vt(out, z);
+#else
+  fe_invert(out, z);
+#endif
+}
+
 // N cached verifications per lane with ONE inversion (Montgomery's trick).
 //   ld.get(j, meta, Aw, Rw, Sw, msg, len, ca)   inputs of signature j
 //   st.put(j, P, prefix) / st.get_point(j, P) /  per-lane stash of R'_j and the
@@ -543,7 +558,7 @@ NT_HD NT_INLINE uint64_t verify_cached_batch(const Loader& ld, const WCombB& cb,
     st.put(j, P2, acc);
   }
   fe inv;
-  fe_invert(inv, acc);
+  fe_invert_batch(inv, acc);
 #pragma unroll 1
   for (int j = m - 1; j >= 0; --j) {
     ge_p2 P;

@@ -50,10 +50,15 @@ struct KsPlan {
 // of a chunk's, and at any moment the grid works on ~`waves` consecutive rows of
 // the key-grouped order (a few committee keys' combs instead of all of them).
 // prow = the average rows per wave + 2 (<= cap): a wave that fills its stash
-// inverts and starts another batch.
+// inverts and starts another batch.  Waves per SIMD: 3 when that still leaves
+// >= 16 rows per wave, else 2 (interleaved A/B, profiles/r03/ab_inv_sort: 3
+// waves +0.7 % on config 3's one-GPU launch (35 rows per wave) and +0.3 % on
+// the 2-GPU shard, -0.5 / -1.3 % on the 4- and 8-GPU shards, where a third
+// wave's inversion is shared by only 9 / 4 rows).
 inline KsPlan ks_stream_plan(uint64_t n, uint32_t cus, uint32_t cap, int force_per_simd) {
   const uint64_t rows = (n + 63) / 64;
-  const uint32_t per = force_per_simd ? (uint32_t)force_per_simd : 2u;
+  const uint32_t per = force_per_simd ? (uint32_t)force_per_simd
+                                      : (rows >= (uint64_t)16 * 3 * 4 * (cus ? cus : 1) ? 3u : 2u);
   const uint64_t slots = (uint64_t)per * 4 * (cus ? cus : 1);
   const uint64_t W = rows < slots ? rows : slots;
   KsPlan p{(uint32_t)W, 0, 0, 0, per, 1};

@@ -12,6 +12,7 @@
 #include <unordered_map>
 
 #include "../../narwhal-tusk_amd/csrc/ed25519_ops.hpp"
+#include "../../narwhal-tusk_amd/csrc/fe_inv_vt.hpp"
 #include "../../narwhal-tusk_amd/csrc/ks_plan.hpp"
 
 namespace nt {
@@ -381,5 +382,46 @@ void nth_ks_plan(unsigned long long n, uint32_t cus, uint32_t cap, int force, ui
 void nth_ks_stream_plan(unsigned long long n, uint32_t cus, uint32_t cap, int force, uint32_t* out) {
   const KsPlan p = ks_stream_plan(n, cus, cap, force);
   out[0] = p.waves; out[1] = p.rows; out[2] = p.prow; out[3] = p.per_simd;
+}
+// field inversion: Fermat (fe_invert) and the variable-time binary GCD (fe_invert_vt); limbs in, canonical bytes out
+void nth_fe_invert(const uint32_t* f, uint8_t* out32, int vt) {
+  fe a, r;
+  std::memcpy(a.v, f, 40);
+  if (vt) fe_invert_vt(r, a);
+  else fe_invert(r, a);
+  uint32_t w[8];
+  fe_tobytes_w(w, r);
+  std::memcpy(out32, w, 32);
+}
+// n pseudo-random inputs (xorshift from seed; 4 in 8 structured: small, near p, powers of two,
+// p + s as a non-canonical encoding) within fe_invert's input contract: number whose two inversions differ
+unsigned long long nth_fe_invert_cmp(unsigned long long n, unsigned long long seed) {
+  unsigned long long bad = 0, x = seed | 1;
+  auto rnd = [&x]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+  for (unsigned long long i = 0; i < n; ++i) {
+    fe a;
+    const uint64_t r0 = rnd();
+    const int kind = (int)(r0 & 7);
+    for (int l = 0; l < 10; ++l) a.v[l] = (uint32_t)rnd() & ((l & 1) ? NT_M25 : NT_M26);
+    if (kind == 1) {  // small: < 2^64
+      for (int l = 3; l < 10; ++l) a.v[l] = 0;
+      a.v[2] &= 0x3fffu;
+    } else if (kind == 2) {  // p - small
+      a.v[0] = NT_M26 - 18u - (uint32_t)(rnd() & 0xffff);
+      for (int l = 1; l < 10; ++l) a.v[l] = (l & 1) ? NT_M25 : NT_M26;
+    } else if (kind == 3) {  // a power of two (or zero)
+      for (int l = 0; l < 10; ++l) a.v[l] = 0;
+      const int l = (int)(rnd() % 10);
+      a.v[l] = 1u << (rnd() % ((l & 1) ? 25 : 26));
+    } else if (kind == 4) {  // p + s, s < 19: reduced-size limbs, non-canonical value (= s)
+      a.v[0] = NT_M26 - 18u + (uint32_t)(rnd() % 19);
+      for (int l = 1; l < 10; ++l) a.v[l] = (l & 1) ? NT_M25 : NT_M26;
+    }
+    uint8_t o1[32], o2[32];
+    nth_fe_invert(a.v, o1, 0);
+    nth_fe_invert(a.v, o2, 1);
+    bad += std::memcmp(o1, o2, 32) != 0;
+  }
+  return bad;
 }
 }

@@ -272,6 +272,39 @@ def test_sign_fixture_through_device_code():
         assert sig.hex() == s
 
 
+def _invert(limbs, vt):
+    import ctypes
+    lib = H.load()
+    out = (ctypes.c_uint8 * 32)()
+    lib.nth_fe_invert((ctypes.c_uint32 * 10)(*limbs), out, vt)
+    return int.from_bytes(bytes(out), "little")
+
+
+def test_fe_invert_vt_vs_fermat_and_bigint():
+    """The key-cache kernel's variable-time inversion (fe_inv_vt.hpp: Pornin's
+    optimized binary GCD, 17 x 30 steps on 62-bit approximations) equals
+    z^(p-2) mod p (Python big integers) on edge values and random inputs, and
+    equals the Fermat chain (fe_invert) on 200k more inputs drawn in the C
+    harness (half of them structured: small, p - small, powers of two, p + s
+    as a non-canonical encoding)."""
+    import ctypes
+    P = H.P
+    rng = random.Random(11)
+    vals = [0, 1, 2, 3, 19, P - 1, P - 2, P + 1, P + 18, 2 ** 254, 2 ** 255 - 20, 2 ** 128, 2 ** 128 - 1,
+            (P - 1) // 2, (P + 1) // 2, 2 ** 62, 2 ** 62 - 1, 2 ** 30, 2 ** 31 + 1]
+    vals += [1 << k for k in range(255)]
+    vals += [P - (1 << k) for k in range(1, 254)]
+    vals += [rng.randrange(P) for _ in range(3000)]
+    vals += [rng.randrange(1 << rng.randrange(1, 255)) for _ in range(1000)]
+    for v in vals:
+        limbs = H.to_limbs(v)
+        want = pow(v % P, P - 2, P)
+        assert _invert(limbs, 1) == want, hex(v)
+    lib = H.load()
+    lib.nth_fe_invert_cmp.restype = ctypes.c_ulonglong
+    assert lib.nth_fe_invert_cmp(ctypes.c_ulonglong(200_000), ctypes.c_ulonglong(0x9E3779B97F4A7C15)) == 0
+
+
 def test_opcount_matches_committed_profile():
     """profiles/opcount.json (roofline numerator) must match the current code."""
     path = os.path.join(os.path.dirname(GOLD), "..", "profiles", "opcount.json")

@@ -93,7 +93,7 @@ def test_stream_plan_invariants(cus):
             for force in (0, 2, 3):
                 p = stream_plan(n, cus, cap, force)
                 rows = (n + 63) // 64
-                per = force or 2
+                per = force or (3 if rows >= 16 * 12 * cus else 2)
                 assert p["per_simd"] == per
                 assert p["rows"] == rows
                 assert p["waves"] == min(rows, per * 4 * cus)
@@ -105,9 +105,9 @@ def test_stream_plan_invariants(cus):
 
 def test_stream_plan_config3_shards():
     """Config 3 (100k certificates x 68 signatures) and its 2/4/8-GPU shards:
-    2 waves per SIMD, one inversion per wave (the stash holds every row a wave
-    takes, with two rows to spare)."""
-    for certs in (100_000, 50_000, 25_000, 12_500):
+    3 waves per SIMD on 1 and 2 GPUs (35 / 17 rows per wave), 2 on 4 and 8, one
+    inversion per wave (the stash holds every row a wave takes, two to spare)."""
+    for certs, waves in ((100_000, 3072), (50_000, 3072), (25_000, 2048), (12_500, 2048)):
         p = stream_plan(certs * 68)
-        assert p["waves"] == 2048
-        assert p["prow"] == math.ceil(p["rows"] / 2048) + 2 <= 64
+        assert p["waves"] == waves
+        assert p["prow"] == math.ceil(p["rows"] / waves) + 2 <= 64

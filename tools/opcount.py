@@ -59,7 +59,8 @@ def measure():
     out["verify_sha512_blocks_512B_msg"] = (64 + 512 + 17 + 127) // 128
     out["note"] = ("host-compiled device code as the kernels run it (verify: two signatures per lane, "
                    "averaged over %d pairs, per-signature = pair / 2; key cache: 8 per lane sharing one "
-                   "inversion); B comb %d bits, key combs %d bits; fe_mul = 100 v_mad_u64_u32, fe_sq = 55; "
+                   "variable-time binary-GCD inversion, whose 17 x 72 v_mad_i64_i32 + 1 fe_mul per batch are "
+                   "not field multiplies and are not counted beyond that fe_mul); B comb %d bits, key combs %d bits; fe_mul = 100 v_mad_u64_u32, fe_sq = 55; "
                    "table builds (wide combs) excluded" % (NPAIRS, H.bcomb_bits(), 20))
     return out
 
