@@ -1323,7 +1323,7 @@ def bench_ingest(args, be, world, rank, local, max_over_ranks, barrier):
               "note": "Core::ingest_device: wire bytes copied as-is (pinned), parsed / checked on the GPU "
                       "(k_cert_parse, k_cert_scatter, one SHA-512 + one NT_MODE_MIXED key-cache launch + group AND "
                       "per chunk of %s messages, chunks alternating two streams so the PCIe copy of one runs under "
-                      "the previous one's kernels); PCIe-inclusive" % os.environ.get("NT_INGEST_CHUNK", "25000")}
+                      "the previous one's kernels); PCIe-inclusive" % os.environ.get("NT_INGEST_CHUNK", "6250")}
     return {"value": device["certs_per_s"], "unit": "certificates/s",
             "path": "device parse (Core::ingest_device); host_decode = the host decoder path",
             "device_parse": device,

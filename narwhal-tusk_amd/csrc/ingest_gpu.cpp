@@ -99,7 +99,7 @@ int grow(DevBuf& b, size_t bytes, hipStream_t s) {
 
 uint64_t chunk_msgs() {
   const char* e = std::getenv("NT_INGEST_CHUNK");
-  const long long v = e ? std::atoll(e) : 25000;
+  const long long v = e ? std::atoll(e) : 6250;
   return (uint64_t)std::max(64ll, v);
 }
 
