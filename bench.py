@@ -878,8 +878,11 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, stream, barri
     key-cache launch, group AND; consecutive steps on two streams with their
     own buffers), timed the same way.  `per_gpu_vs_1gpu` = this shard's
     certificates/s on one GPU / the full batch's: what each GPU of an N-GPU run
-    keeps of the 1-GPU rate (the key-cache launch plan, ks_plan.hpp, sizes the
-    persistent grid and chunks to the shard)."""
+    keeps of the 1-GPU rate (the key-cache launch plan, ks_stream_plan in
+    ks_plan.hpp, sizes the persistent grid to the shard; its waves stream rows).
+    `expected_aggregate_certs_per_s` = N x that rate: the strong-scaled N-GPU
+    aggregate this GPU's shard rate implies (the 8-GPU run itself is the
+    driver's)."""
     res = {}
     steps = max(1, min(args.steps, 5))
     nst = len(streams)
@@ -948,7 +951,8 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, stream, barri
                        "ms_per_step": round(wall * 1e3 / steps, 3),
                        "gpu_ms_per_step": round(ev0.elapsed_time(ev1) / steps, 3),
                        "keyset_launch_ms": round(float(np.mean([a.elapsed_time(b) for a, b in kev])), 3),
-                       "per_gpu_vs_1gpu": round(rate / rate1, 3), "mismatches_vs_expected": bad}
+                       "per_gpu_vs_1gpu": round(rate / rate1, 3),
+                       "expected_aggregate_certs_per_s": round(N * rate, 1), "mismatches_vs_expected": bad}
     res["note"] = ("one GPU running the first G/N certificates of the same batch, as rank r of an N-GPU run would "
                    "(nd.shard); per_gpu_vs_1gpu >= 0.9 means the N-GPU aggregate stays within 10% of linear")
     return res

@@ -404,3 +404,45 @@ def test_verify_ragged_message_lengths(be, oracle):
     for i in rng.choice(n, 64, replace=False):
         m = data[int(off[i]):int(off[i] + lens[i])].tobytes()
         assert cof[i] == oracle.verify_cofactorless(pk[i].tobytes(), sig[i].tobytes(), m), int(i)
+
+
+@pytest.mark.timeout(300)
+def test_keyset_device_api_two_launches(be, corpus, monkeypatch):
+    """More than kKsMaxPerLaunch (8M) signatures in one device-API call: the
+    launcher cuts them into an 8M launch and a 0.53M one that reuse one stash
+    (sized for the larger of the two streamed-row plans: 3 waves per SIMD x 45
+    rows, then 2 x 7) and one key-sort scratch.  The corpus tiled to ~8.53M
+    signatures in mixed mode (every edge case, per-signature strictness,
+    unknown keys) must give the corpus labels everywhere."""
+    import ntcrypto
+    import torch
+    monkeypatch.setenv("NT_KEYSET_COMB_BITS", "16")
+    uniq, inv = np.unique(corpus["pk"], axis=0, return_inverse=True)
+    inv = inv.ravel().astype(np.uint32)
+    ks = be.keyset(uniq)
+    n0 = len(inv)
+    reps = -(-((8 << 20) + 530_000) // n0)
+    n = n0 * reps
+    i = np.arange(n)
+    unknown = (i % 97) == 5
+    strict = (i % 3) == 1
+    idx = np.tile(inv, reps)
+    idx[unknown] = len(uniq) + 3
+    midx = (idx | np.where(strict, np.uint32(ntcrypto.NT_KEY_STRICT_BIT), np.uint32(0))).astype(np.uint32)
+    want = np.where(strict, np.tile(corpus["strict"], reps), np.tile(corpus["batch_rule"], reps)).astype(bool)
+    want &= ~unknown
+    dev = torch.device("cuda", 0)
+    t = {"k": torch.from_numpy(midx.view(np.int32)).to(dev),
+         "sig": torch.from_numpy(np.ascontiguousarray(corpus["sig"])).to(dev).repeat(reps, 1),
+         "msg": torch.from_numpy(np.ascontiguousarray(corpus["msg"])).to(dev),
+         "off": torch.from_numpy(np.ascontiguousarray(corpus["off"]).view(np.int64)).to(dev).repeat(reps),
+         "len": torch.from_numpy(np.ascontiguousarray(corpus["len"]).view(np.int64)).to(dev).repeat(reps)}
+    out = torch.zeros((n + 63) // 64 + 1, dtype=torch.int64, device=dev)
+    st = torch.cuda.Stream(dev)
+    ks.dev_verify(0, st.cuda_stream, ntcrypto.NT_MODE_MIXED, t["k"].data_ptr(), t["sig"].data_ptr(),
+                  t["msg"].data_ptr(), t["off"].data_ptr(), t["len"].data_ptr(), n, out.data_ptr())
+    st.synchronize()
+    got = np.unpackbits(out.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+    assert n > (8 << 20)
+    assert int((got != want).sum()) == 0
+    ks.close()

@@ -1,0 +1,7 @@
+# round 3 (session 2): final validation of the tree -- full GPU suite, smoke, two default bench runs
+set -o pipefail
+mkdir -p gpurun_out/r03x
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread --durations 10 > gpurun_out/r03x/tests.log 2>&1 || exit 1
+timeout -k 10 240 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03x/smoke.log 2>&1 || exit 1
+timeout -k 10 300 python -u bench.py > gpurun_out/r03x/bench1.log 2>&1 || exit 1
+timeout -k 10 300 python -u bench.py > gpurun_out/r03x/bench2.log 2>&1
