@@ -309,10 +309,14 @@ def test_keyset_per_lane_counts():
     import subprocess
     import sys
     probe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_keyset_per_lane_probe.py")
-    cases = [("1", 1, ""), ("1", 3, "3"), ("1", 8, "2"), ("1", 64, ""), ("1", 64, "3"),
-             ("0", 1, ""), ("0", 5, "2"), ("0", 8, "3"), ("0", 26, "2"), ("0", 64, "")]
-    for stream, m, w in cases:
-        env = dict(os.environ, NT_KEYSET_PER_LANE=str(m), NT_KEYSET_COMB_BITS="16", NT_KEYSET_STREAM=stream)
+    # (stream, rows per inversion, waves per SIMD, key-grouped order); sort "0" = input order at every
+    # size (the streamed kernel's ballot verdict path at ~1M signatures)
+    cases = [("1", 1, "", "1"), ("1", 3, "3", "1"), ("1", 8, "2", "1"), ("1", 64, "", "1"), ("1", 64, "3", "1"),
+             ("1", 64, "", "0"), ("1", 5, "3", "0"),
+             ("0", 1, "", "1"), ("0", 5, "2", "1"), ("0", 8, "3", "1"), ("0", 26, "2", "1"), ("0", 64, "", "1")]
+    for stream, m, w, srt in cases:
+        env = dict(os.environ, NT_KEYSET_PER_LANE=str(m), NT_KEYSET_COMB_BITS="16", NT_KEYSET_STREAM=stream,
+                   NT_KEYSET_SORT=srt)
         env.pop("NT_KEYSET_WAVES", None)
         if w:
             env["NT_KEYSET_WAVES"] = w
