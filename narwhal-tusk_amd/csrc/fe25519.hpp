@@ -34,10 +34,17 @@ namespace nt { extern unsigned long long g_fe_mul, g_fe_sq; }
 // Scheduling fence after each multiply: the 10 column chains inside one mul
 // are enough ILP for a wave; letting the scheduler overlap several muls only
 // multiplies register pressure (spills, lower occupancy).
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(NT_NO_MUL_FENCE)
+// -DNT_FENCE_POINT (A/B builds): fence after each point operation instead, so
+// the 3-4 independent multiplies of one formula may interleave.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(NT_NO_MUL_FENCE) && !defined(NT_FENCE_POINT)
 #define NT_MUL_FENCE() __builtin_amdgcn_sched_barrier(0)
 #else
 #define NT_MUL_FENCE() ((void)0)
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && defined(NT_FENCE_POINT)
+#define NT_POINT_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define NT_POINT_FENCE() ((void)0)
 #endif
 
 // Pins a value as a 32-bit VGPR (no instruction emitted).  Without it LLVM

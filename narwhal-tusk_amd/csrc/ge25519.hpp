@@ -37,12 +37,14 @@ NT_HD NT_INLINE void ge_cp_to_p2(ge_p2& r, const ge_cp& p) {
   fe_mul(r.X, p.T, p.X);
   fe_mul(r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.T, p.Z);
+  NT_POINT_FENCE();
 }
 NT_HD NT_INLINE void ge_cp_to_p3(ge_p3& r, const ge_cp& p) {
   fe_mul(r.X, p.T, p.X);
   fe_mul(r.Y, p.Y, p.Z);
   fe_mul(r.Z, p.T, p.Z);
   fe_mul(r.T, p.Y, p.X);
+  NT_POINT_FENCE();
 }
 NT_HD NT_INLINE void ge_p3_to_p2(ge_p2& r, const ge_p3& p) { r.X = p.X; r.Y = p.Y; r.Z = p.Z; }
 
@@ -66,6 +68,7 @@ NT_HD NT_INLINE void ge_p3_to_cached(ge_cached& r, const ge_p3& p) {
   fe_carry(r.Z2);
 #endif
   fe_mul(r.T2d, p.T, d2);
+  NT_POINT_FENCE();
 }
 
 // 2P from a p2 point with "R" coordinates (dalek ProjectivePoint::double).
@@ -89,6 +92,7 @@ NT_HD NT_INLINE void ge_dbl(ge_cp& r, const ge_p2& p) {
   fe_add(ZZ, ZZ, ZZ);
   fe_sub4(r.T, ZZ, r.Z);
 #endif
+  NT_POINT_FENCE();
 }
 
 // P + Q (neg=0) or P - Q (neg=1), Q cached with "R" coordinates.
@@ -104,6 +108,7 @@ NT_HD NT_INLINE void ge_add_cached(ge_cp& r, const ge_p3& p, const ge_cached& q)
   fe_add(r.Y, PP, MM);
   fe_add(r.Z, ZZ, TT);
   fe_sub(r.T, ZZ, TT);
+  NT_POINT_FENCE();
 }
 
 // P + Q, Q affine niels.  Split in two halves so a caller can issue its next
@@ -115,6 +120,7 @@ NT_HD NT_INLINE void ge_add_niels_1(fe& PP, fe& MM, fe& TT, const ge_p3& p, cons
   fe_mul(PP, a, q.ypx);
   fe_mul(MM, b, q.ymx);
   fe_mul(TT, p.T, q.xy2d);
+  NT_POINT_FENCE();
 }
 NT_HD NT_INLINE void ge_add_niels_2(ge_cp& r, const fe& PP, const fe& MM, const fe& TT, const fe& Z) {
   fe ZZ;
@@ -123,6 +129,7 @@ NT_HD NT_INLINE void ge_add_niels_2(ge_cp& r, const fe& PP, const fe& MM, const 
   fe_add(r.Y, PP, MM);
   fe_add(r.Z, ZZ, TT);
   fe_sub(r.T, ZZ, TT);        // ZZ + 2p - TT < 2^27.6
+  NT_POINT_FENCE();
 }
 NT_HD NT_INLINE void ge_add_niels(ge_cp& r, const ge_p3& p, const ge_niels& q) {
   fe PP, MM, TT;
@@ -143,6 +150,7 @@ NT_HD NT_INLINE void ge_p3_from_niels(ge_p3& r, const ge_niels& q) {
   fe_0(r.Z);
   r.Z.v[0] = 2;
   fe_mul(r.T, q.xy2d, dinv);  // xy2d: niels (< 2^26) or its fe_neg (f side)
+  NT_POINT_FENCE();
 }
 
 // Affine niels entry of the projective point (X:Y:Z), given zi = Z^-1.
@@ -157,6 +165,7 @@ NT_HD NT_INLINE void ge_niels_from(ge_niels& q, const fe& X, const fe& Y, const 
   fe_const(d2, kFeD2);
   fe_mul(q.xy2d, x, y);
   fe_mul(q.xy2d, q.xy2d, d2);
+  NT_POINT_FENCE();
 }
 
 // Conditionally negate a cached entry in place: -(Y+X, Y-X, 2Z, 2dT) = (Y-X, Y+X, 2Z, -2dT)
