@@ -412,18 +412,13 @@ constexpr uint64_t kKsMaxPerLaunch = 8ull << 20;
 constexpr uint32_t kSortBuckets = 4096;  // committee keys + 1 "unknown" bucket
 constexpr uint64_t kSortMin = 65536;     // smaller launches keep the input order
 constexpr int kSortTile = 16;            // items per thread of k_key_scatter
-// -DNT_SORT_LEGACY=1 (A/B builds): round-2 histogram (one key per loop iteration, 64 per
-// thread, <= 1024 blocks) and packed counters
-#ifndef NT_SORT_LEGACY
-#define NT_SORT_LEGACY 0
-#endif
-constexpr int kHistTile = NT_SORT_LEGACY ? 1 : 16;  // independent key loads in flight per thread of k_key_hist
+constexpr int kHistTile = 16;            // independent key loads in flight per thread of k_key_hist
 // Global bucket counters one 128-B line apart: every block's flush / reservation
 // is one device-scope atomic per bucket, and with the counters packed 32 to a
 // line those atomics serialize per LINE (rocprof r03b: k_key_scatter 66 us at
 // 1,661 blocks, ~1.6 ns per atomic on one of 4 lines; k_key_hist 43 us whatever
 // the size, one dependent load + LDS atomic per loop iteration).
-constexpr uint32_t kCtrStride = NT_SORT_LEGACY ? 1 : 32;
+constexpr uint32_t kCtrStride = 32;
 
 NT_D NT_INLINE uint32_t sort_bucket(uint32_t k, int mixed, uint32_t nkeys) {
   if (mixed) k &= ~kKeyWantStrict;
@@ -452,14 +447,21 @@ __global__ __launch_bounds__(kBlock) void k_key_hist(const uint32_t* __restrict_
     if (h[b]) atomicAdd(&hist[b * kCtrStride], h[b]);
 }
 
-// exclusive scan of nb <= kSortBuckets counts (one workgroup; ~4k adds)
-__global__ __launch_bounds__(kBlock) void k_key_scan(const uint32_t* __restrict__ hist, uint32_t nb,
-                                                    uint32_t* __restrict__ cursor) {
+// Each block computes the exclusive prefix of the global histogram itself (the
+// counts are final: k_key_hist ran before on the stream) and reserves its
+// ranges with one atomic per bucket on the bucket line's second word (zeroed
+// with the histogram by one memset): no separate scan launch.
+__global__ __launch_bounds__(kBlock) void k_key_scatter(const uint32_t* __restrict__ key, uint64_t n, int mixed,
+                                                       uint32_t nkeys, uint32_t* __restrict__ lines,
+                                                       uint32_t* __restrict__ perm) {
+  __shared__ uint32_t cnt[kSortBuckets];
+  __shared__ uint32_t base[kSortBuckets];
   __shared__ uint32_t part[kBlock];
-  const uint32_t per = (nb + kBlock - 1) / kBlock, b0 = threadIdx.x * per;
+  const uint32_t nb = nkeys + 1, per = (nb + kBlock - 1) / kBlock, b0 = threadIdx.x * per;
   uint32_t sum = 0;
-  for (uint32_t b = b0; b < b0 + per && b < nb; ++b) sum += hist[b * kCtrStride];
+  for (uint32_t b = b0; b < b0 + per && b < nb; ++b) sum += lines[b * kCtrStride];
   part[threadIdx.x] = sum;
+  for (uint32_t b = threadIdx.x; b <= nkeys; b += kBlock) cnt[b] = 0;
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t acc = 0;
@@ -470,20 +472,13 @@ __global__ __launch_bounds__(kBlock) void k_key_scan(const uint32_t* __restrict_
     }
   }
   __syncthreads();
-  uint32_t acc = part[threadIdx.x];
-  for (uint32_t b = b0; b < b0 + per && b < nb; ++b) {
-    cursor[b * kCtrStride] = acc;
-    acc += hist[b * kCtrStride];
+  {
+    uint32_t acc = part[threadIdx.x];
+    for (uint32_t b = b0; b < b0 + per && b < nb; ++b) {
+      base[b] = acc;
+      acc += lines[b * kCtrStride];
+    }
   }
-}
-
-__global__ __launch_bounds__(kBlock) void k_key_scatter(const uint32_t* __restrict__ key, uint64_t n, int mixed,
-                                                       uint32_t nkeys, uint32_t* __restrict__ cursor,
-                                                       uint32_t* __restrict__ perm) {
-  __shared__ uint32_t cnt[kSortBuckets];
-  __shared__ uint32_t base[kSortBuckets];
-  for (uint32_t b = threadIdx.x; b <= nkeys; b += kBlock) cnt[b] = 0;
-  __syncthreads();
   const uint64_t t0 = (uint64_t)blockIdx.x * kBlock * kSortTile;
   uint32_t bk[kSortTile], rk[kSortTile];
 #pragma unroll
@@ -494,7 +489,7 @@ __global__ __launch_bounds__(kBlock) void k_key_scatter(const uint32_t* __restri
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b <= nkeys; b += kBlock)
-    if (cnt[b]) base[b] = atomicAdd(&cursor[b * kCtrStride], cnt[b]);
+    if (cnt[b]) base[b] += atomicAdd(&lines[b * kCtrStride + 1], cnt[b]);
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < kSortTile; ++r) {
@@ -520,11 +515,12 @@ static bool keyset_sort_enabled() {
   return on;
 }
 
-// d_sort layout: [16 words: row / chunk counter][hist 4096 x 32][cursor 4096 x 32][perm m][verdict bytes m]
+// d_sort layout: [16 words: row / chunk counter][4096 bucket lines of 32 words: word 0 the
+// histogram count, word 1 the scatter's reservation counter][perm m][verdict bytes m]
 constexpr size_t kSortHdr = 64;
 size_t keyset_sort_bytes(uint64_t n) {
   const uint64_t m = n < kKsMaxPerLaunch ? n : kKsMaxPerLaunch;
-  return kSortHdr + 2 * (size_t)kSortBuckets * kCtrStride * 4 + (size_t)m * 5 + 64;
+  return kSortHdr + (size_t)kSortBuckets * kCtrStride * 4 + (size_t)m * 5 + 64;
 }
 
 // NT_KEYSET_STREAM=0 selects the chunked plan (ks_plan) instead of streamed rows
@@ -550,29 +546,27 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
   if (!d_sort || !d_stash) return hipErrorInvalidValue;
   uint32_t* ctr = (uint32_t*)d_sort;
   uint32_t* hist = ctr + kSortHdr / 4;
-  uint32_t* cursor = hist + kSortBuckets * kCtrStride;
-  uint32_t* p = cursor + kSortBuckets * kCtrStride;
+  uint32_t* p = hist + kSortBuckets * kCtrStride;
   // launches of at most kKsMaxPerLaunch signatures reuse one stash (stream-ordered)
   for (uint64_t lo = 0; lo < n; lo += kKsMaxPerLaunch) {
     const uint64_t m = n - lo < kKsMaxPerLaunch ? n - lo : kKsMaxPerLaunch;
     const KsPlan pl = keyset_plan(m, cus);
     const uint32_t* perm = nullptr;
     uint8_t* bytes = nullptr;
-    hipError_t e = hipMemsetAsync(ctr, 0, 4, s);
+    const bool sorted = keyset_sort_enabled() && m >= kSortMin && nkeys + 1 <= kSortBuckets;
+    // the row counter, and for a sorted launch the bucket lines (count + reservation), in one memset
+    hipError_t e = hipMemsetAsync(ctr, 0, sorted ? kSortHdr + 4ull * kCtrStride * (nkeys + 1) : 4, s);
     if (e != hipSuccess) return e;
-    if (keyset_sort_enabled() && m >= kSortMin && nkeys + 1 <= kSortBuckets) {
+    if (sorted) {
       bytes = (uint8_t*)(p + m);
       const int mixed = mode == kMixed;
-      if ((e = hipMemsetAsync(hist, 0, 4ull * kCtrStride * (nkeys + 1), s)) != hipSuccess) return e;
       // one tile of kHistTile keys per thread and at most 512 blocks (each flushes its
       // LDS histogram with one global atomic per bucket)
-      const uint64_t per = NT_SORT_LEGACY ? 64 : kHistTile, cap = NT_SORT_LEGACY ? 1024 : 512;
-      const uint64_t hw = (m + (uint64_t)kBlock * per - 1) / ((uint64_t)kBlock * per);
-      const uint32_t hb = (uint32_t)(hw < cap ? hw : cap);
+      const uint64_t hw = (m + (uint64_t)kBlock * kHistTile - 1) / ((uint64_t)kBlock * kHistTile);
+      const uint32_t hb = (uint32_t)(hw < 512 ? hw : 512);
       hipLaunchKernelGGL(k_key_hist, dim3(hb), dim3(kBlock), 0, s, d_key_idx + lo, m, mixed, nkeys, hist);
-      hipLaunchKernelGGL(k_key_scan, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)hist, nkeys + 1, cursor);
       const uint64_t sb = (m + (uint64_t)kBlock * kSortTile - 1) / ((uint64_t)kBlock * kSortTile);
-      hipLaunchKernelGGL(k_key_scatter, dim3((uint32_t)sb), dim3(kBlock), 0, s, d_key_idx + lo, m, mixed, nkeys, cursor,
+      hipLaunchKernelGGL(k_key_scatter, dim3((uint32_t)sb), dim3(kBlock), 0, s, d_key_idx + lo, m, mixed, nkeys, hist,
                          p);
       if ((e = hipGetLastError()) != hipSuccess) return e;
       perm = p;
