@@ -10,7 +10,7 @@
 //                         (per-entry rule of crypto/src/lib.rs:206-219 -> dalek verify_batch,
 //                         SURVEY.md A.3); one verdict bit per signature (64-bit ballot words)
 //   k_ed25519_verify_keyset<M>  the same against a committee key cache (wide combs of -A),
-//                         up to eight signatures per lane sharing one inversion
+//                         persistent waves streaming rows, one (binary-GCD) inversion per wave batch
 //   k_group_and           AND of per-signature bits over each certificate's vote range
 //   k_group_msgs          per-signature message offset/length of certificate groups
 //   k_ed25519_sign        keygen + RFC 8032 signing (corpus generation / SignatureService
