@@ -134,6 +134,38 @@ def full_host(rate, threads, host):
                     "state); an estimate, not a measurement" % (threads, host["nproc"])}
 
 
+def pipeline_streams(torch, be, dev, stream, n):
+    """The n streams consecutive steps alternate between.  n = 2: the library's
+    two compute streams (nt_dev_stream), created on hardware queues of their
+    own -- two torch pool streams can share one queue (HIP multiplexes a
+    process's streams over GPU_MAX_HW_QUEUES = 4), and then their kernels run
+    strictly in order: the round-3 bench's config-3 streams did (rocprofv3
+    kernel trace, profiles/r04/).  NT_BENCH_TORCH_STREAMS=1 (A/B): torch's own."""
+    if n == 1:
+        return [stream]
+    if os.environ.get("NT_BENCH_TORCH_STREAMS") == "1" or not hasattr(be, "dev_stream"):
+        return [stream] + [torch.cuda.Stream(dev) for _ in range(n - 1)]
+    return [torch.cuda.ExternalStream(be.dev_stream(0, k), device=dev) for k in range(n)]
+
+
+def fork_join(streams, stream):
+    """Events that bracket a pipelined region on `stream`: fork() makes every
+    pipeline stream wait for `stream`, join() makes `stream` wait for all of them."""
+    def fork(ev0):
+        for st in streams:
+            if st is not stream:
+                st.wait_event(ev0)
+
+    def join():
+        import torch
+        for st in streams:
+            if st is not stream:
+                j = torch.cuda.Event()
+                j.record(st)
+                stream.wait_event(j)
+    return fork, join
+
+
 def free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -253,7 +285,8 @@ def main():
     # launches are independent) -- measured slower or equal for config 2
     # (DESIGN.md §10), unlike config 3.
     nstreams = 2 if os.environ.get("NT_BENCH_STREAMS", "1") == "2" else 1
-    streams = [stream, torch.cuda.Stream(dev)]
+    streams = pipeline_streams(torch, be, dev, stream, nstreams)
+    fork, join = fork_join(streams, stream)
     outs = [torch.zeros(words, dtype=torch.int64, device=dev) for _ in range(2)]
     out = outs[0]
     lev = []  # per-launch (start, end) events: each launch's own duration (what rocprof reports)
@@ -275,19 +308,19 @@ def main():
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for st in streams[1:nstreams]:
-        st.wait_event(ev0)
+    fork(ev0)
     for i in range(args.steps):
         step(i, timed=True)
-    for st in streams[1:nstreams]:
-        j = torch.cuda.Event()
-        j.record(st)
-        stream.wait_event(j)
+    join()
     ev1.record(stream)
     barrier()
     wall = time.perf_counter() - t0
     step_ms = ev0.elapsed_time(ev1) / args.steps          # per batch, steady state
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in lev]))  # per launch
+    ranks_cfg2 = nd.gather_object({"rank": rank, "device": local, "signatures": n, "kernel_ms": round(kernel_ms, 3),
+                                   "gpu_ms_per_step": round(step_ms, 3),
+                                   "wall_ms_per_step": round(wall * 1e3 / args.steps, 3),
+                                   "rate": round(n * args.steps / wall, 1)})
     wall = max_over_ranks(wall)
     mism = 0
     for o in outs[:min(nstreams, args.steps)]:
@@ -335,7 +368,11 @@ def main():
                 "issue_note": "the kernel is VALU-issue-bound (issue share from the PMC profile); non-mad VALU work "
                               "(carries, pre-scaling, SHA-512, lattice reduction) is why mad frac < issue share"}
 
-    line = {"metric": METRIC, "value": round(value, 1), "unit": "verifies/s", "n_gpus": world,
+    # the other two halves of the metric, filled in when their configs have run, so
+    # that they sit near the front of the line (a reader of its first few hundred
+    # bytes sees all of it): config 4's SHA-512 GB/s and config 3's certificates/s
+    line = {"metric": METRIC, "value": round(value, 1), "unit": "verifies/s", "sha512_gbs": None,
+            "certs_per_s": None, "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 limbs / u64 acc",
             "data": "synthetic (seeded random keys and 512-B messages, GPU-signed; 1% Appendix-B edge cases "
@@ -410,6 +447,20 @@ def main():
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args, pk_h, sig_h, msg_h, L, got)
 
+    if "sha512" in line:
+        line["sha512_gbs"] = line["sha512"]["value"]
+    if "certificates" in line:
+        line["certs_per_s"] = line["certificates"]["value"]
+    if world > 1:
+        # what each rank did and how long it took (gathered outside the timed regions)
+        line["per_rank"] = {"cfg2": nd.rank_summary(ranks_cfg2)}
+        for key, sub in (("cfg4", line.get("sha512")), ("cfg3", line.get("certificates"))):
+            if sub and "_ranks" in sub:
+                line["per_rank"][key] = sub.pop("_ranks")
+    else:
+        for sub in (line.get("sha512"), line.get("certificates")):
+            if sub:
+                sub.pop("_ranks", None)
     if rank == 0:
         print(json.dumps(line), flush=True)
     be.close()
@@ -444,8 +495,12 @@ def bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_r
         step()
     ev1.record(stream)
     barrier()
-    wall = max_over_ranks(time.perf_counter() - t0)
+    wall_r = time.perf_counter() - t0
+    wall = max_over_ranks(wall_r)
     kms = ev0.elapsed_time(ev1) / steps
+    ranks = nd.gather_object({"rank": rank, "messages": m, "kernel_ms": round(kms, 3),
+                              "wall_ms_per_step": round(wall_r * 1e3 / steps, 3),
+                              "rate": round(m * ml * steps / wall_r / 1e9, 2) if wall_r > 0 else 0.0})
     # spot-check 4 digests against hashlib
     import hashlib
     ok = True
@@ -461,7 +516,7 @@ def bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_r
            "hbm_frac": round((m * padded / (kms * 1e-3)) / 1e9 / HBM_PEAK_GBS, 4),
            "valu_issue_share": round(pv["valu_issue_share_4cyc"], 3) if "valu_issue_share_4cyc" in pv else None,
            "note": "k_sha512_pipe: per 64 messages a producer wave expands K+W into LDS, a consumer wave runs the rounds; bound by the consumer wave's serial per-block stream (latency-bound, SURVEY H2), not HBM; valu_issue_share from the PMC profile (256 consumer + 256 producer waves on 1,024 SIMDs)",
-           "spot_check_ok": bool(ok)}
+           "spot_check_ok": bool(ok), "_ranks": nd.rank_summary(ranks)}
     # the shards one GPU holds when config 4 runs on N = 2 / 4 / 8 GPUs: each is
     # timed on this GPU, and the N-GPU aggregate follows as N x its per-GPU rate.
     # A lane per message is bound by one lane's serial ~3,907-block chain, so the
@@ -710,7 +765,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
     # independent); NT_BENCH_STREAMS=1: one stream.  The uncached reference runs
     # on one stream.
     nst = 2 if os.environ.get("NT_BENCH_STREAMS", "2") != "1" else 1
-    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(nst - 1)]
+    streams = pipeline_streams(torch, be, dev, stream, nst)
 
     def make_bufs():
         b = {"hd2": torch.empty((G, 32), dtype=torch.uint8, device=dev),
@@ -812,20 +867,22 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
         barrier()
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
+        fork, join = fork_join(streams[:slots(cached)], stream)
         t0 = time.perf_counter()
         ev0.record(stream)
-        for st in streams[1:slots(cached)]:
-            st.wait_event(ev0)
+        fork(ev0)
         for i in range(steps):
             step(cached, i, timed=True)
-        for st in streams[1:slots(cached)]:
-            j = torch.cuda.Event()
-            j.record(st)
-            stream.wait_event(j)
+        join()
         ev1.record(stream)
         barrier()
-        wall = max_over_ranks(time.perf_counter() - t0)
+        wall_r = time.perf_counter() - t0
+        wall = max_over_ranks(wall_r)
         kms = ev0.elapsed_time(ev1) / steps
+        if key == "keyset":
+            ranks3 = nd.gather_object({"rank": rank, "certificates": G, "signatures": G * (quorum + 1),
+                                       "kernel_ms": round(kms, 3), "wall_ms_per_step": round(wall_r * 1e3 / steps, 3),
+                                       "rate": round(G * steps / wall_r, 1)})
         bad = sum(int((verdicts(cached, k) != expect).sum()) for k in range(min(slots(cached), steps)))
         mism = int(max_over_ranks(bad))
         out[key] = {"certs_per_s": round(G_total * steps / wall, 1),
@@ -852,6 +909,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
     ks.close()
     if world == 1 and not getattr(args, "no_cpu", False):
         out["cpu_baseline"] = cert_cpu_baseline(args, hdr, hlen, ids, tmp_pk, hsig, cpre, vpk, vsig, quorum, expect)
+    out["_ranks"] = nd.rank_summary(ranks3)
     return {"value": out["keyset"]["certs_per_s"], "unit": "certificates/s",
             "workload": "cfg3: %d certificates, committee n=%d, %d votes + 1 header signature each, "
                         "%d-byte header preimage" % (G_total, nk, quorum, hlen),
@@ -926,16 +984,13 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, stream, barri
         barrier()
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
+        fork, join = fork_join(streams, stream)
         t0 = time.perf_counter()
         ev0.record(stream)
-        for st in streams[1:]:
-            st.wait_event(ev0)
+        fork(ev0)
         for i in range(steps):
             step(i, timed=True)
-        for st in streams[1:]:
-            j = torch.cuda.Event()
-            j.record(st)
-            stream.wait_event(j)
+        join()
         ev1.record(stream)
         barrier()
         wall = time.perf_counter() - t0

@@ -72,18 +72,42 @@ int nt_init(nt_ctx **out, int num_gpus);
 /* One specific device ordinal (used by one-process-per-GPU launchers). */
 int nt_init_device(nt_ctx **out, int device_ordinal);
 /* An explicit list of device ordinals; repeats are allowed (each entry gets
- * its own stream, tables and workspace), which lets the multi-device sharding
- * of the host entry points be exercised on a single GPU.
- * Device memory: the wide comb of B (24-bit digits, 11.8 GB; 872 MB in a
- * -DNT_BCOMB_BITS=20 build) once per device ordinal per process, shared by
- * every entry and context on that ordinal; per entry the verify workspace
- * (~1.5 GB at 2,048 slots) + grow-only staging. */
+ * its own streams, workspace and staging), which lets the multi-device
+ * sharding of the host entry points be exercised on a single GPU. */
 int nt_init_devices(nt_ctx **out, const int *ordinals, int n);
 void nt_free(nt_ctx *ctx);
 int nt_num_devices(const nt_ctx *ctx);
 const char *nt_strerror(int code);
 /* Library / build identification, e.g. "ntcrypto 0.1 gfx950". */
 const char *nt_version(void);
+
+/* ---- device memory (lazy, budgeted) -----------------------------------
+ * The reference runs every primary and every worker as its own process
+ * (node/src/main.rs:101-133); a worker only hashes (worker/src/processor.rs:38).
+ * So nt_init allocates nothing large: a context that only digests holds
+ * streams and grow-only staging.  The first call that verifies or signs on a
+ * device entry builds the wide comb of B there (shared by every context of
+ * the process on that ordinal and width) and, for the verify kernel, the [k]A
+ * workspace (~1.5 GB per execution slot that verifies).  The comb's width is
+ * the widest that fits: 24-bit digits (11 additions per [s]B, 11.8 GB) when
+ * the context's budget allows it and the device keeps 4 GB free beside it,
+ * else 20-bit digits (13 additions, 872 MB); NT_BCOMB_BITS=24|20 forces one.
+ * A key set (nt_keyset_create) reserves its key combs against the same budget
+ * after the comb of B: 20 / 18 / 16-bit digits, the widest that fits.
+ *
+ * nt_set_hbm_budget: bytes of such TABLES (comb of B + key combs) the context
+ * may hold per device entry; 0 = no cap (the device's free memory decides).
+ * Default: the NT_HBM_BUDGET environment variable at nt_init (bytes, or with a
+ * K / M / G suffix).  Applies to the tables built after the call; NT_ENOMEM
+ * when not even the narrowest width fits.
+ *
+ * nt_memory_info(ctx, dev, out8): what device entry `dev` of THIS context holds:
+ *   out8[0] comb of B digit width (0 = not built yet)   out8[1] its bytes
+ *   out8[2] key-comb bytes of live key sets             out8[3] verify workspaces
+ *   out8[4] key-cache stashes + sort scratch            out8[5] other device staging
+ *   out8[6] the budget (0 = none)                       out8[7] table bytes held against it */
+int nt_set_hbm_budget(nt_ctx *ctx, uint64_t bytes_per_device);
+int nt_memory_info(nt_ctx *ctx, int dev, uint64_t *out8);
 
 /* SHA-512 truncated to 32 bytes of n independent messages packed in `data`
  * (message i = data[off[i] .. off[i] + len[i])).  out32: n * 32 bytes. */
@@ -115,16 +139,20 @@ int nt_ed25519_keypair_batch(nt_ctx *ctx, const uint8_t *seed32, uint64_t n, uin
 /* ---- committee key cache ------------------------------
  * A keyset holds, on every device of the context, per-key comb tables
  * (the wide comb of -A: 20-bit digits, 13 x 524289 affine niels entries =
- * 872 MB per key when every device can hold them with 1/8 of its HBM to
- * spare -- 87 GB for n = 100 -- else 16-bit digits, 16 x 32769 entries =
- * 67 MB per key; NT_KEYSET_COMB_BITS=16|18|20 forces one -- 18 bits: 15 x
- * 131073 entries = 252 MB per key) plus each key's raw
+ * 872 MB per key -- 87 GB for n = 100 -- when every device can hold them
+ * with 1/8 of its HBM to spare and the context's HBM budget allows, else
+ * 18-bit digits, 15 x 131073 entries = 252 MB per key, else 16-bit digits,
+ * 16 x 32769 entries = 67 MB per key; NT_KEYSET_COMB_BITS=16|18|20 forces
+ * one) plus each key's raw
  * encoding and decode / small-order flags, so verification against a static
  * committee (config/src/lib.rs:140-143) needs no decompression of A and no
  * doublings.  Keys are addressed by index (the caller's committee order);
  * an index >= nkeys means "not a committee key" and verifies as reject.
  * Keys that do not decode are accepted into the set and always reject, as
- * PublicKey::from_bytes would (crypto/src/lib.rs:202,216). */
+ * PublicKey::from_bytes would (crypto/src/lib.rs:202,216).
+ * Lifetime: free every keyset before its context; an nt_committee built on a
+ * keyset keeps the keyset's device tables alive, so the keyset handle may be
+ * freed before the committee. */
 typedef struct nt_keyset nt_keyset;
 int nt_keyset_create(nt_ctx *ctx, const uint8_t *pk32, uint32_t nkeys, nt_keyset **out);
 void nt_keyset_free(nt_keyset *ks);
@@ -154,8 +182,14 @@ int nt_ed25519_verify_batch_groups_keyset(nt_ctx *ctx, const nt_keyset *ks, cons
  * nt_committee: the committee of a keyset (key i = keyset key i): stake per
  * key, its worker ids (worker_ids[worker_first[i] .. worker_first[i + 1]),
  * any order) and the quorum threshold (config/src/lib.rs:168-173:
- * 2 * total_stake / 3 + 1).  Keys are looked up by their canonical base64
- * text (crypto/src/lib.rs:73-79,103-112), as the reference's serde does. */
+ * 2 * total_stake / 3 + 1).  The keyset's keys ARE the committee's
+ * authorities (Committee::authorities, config/src/lib.rs:140-143): build it
+ * from exactly those keys.  Certificate::genesis(committee) has one
+ * certificate per authority (primary/src/messages.rs:175-187), so a round-0
+ * certificate with the zero header id whose author is a keyset key is
+ * genesis, whatever that key's stake -- as in the reference.  Keys are
+ * looked up by their canonical base64 text (crypto/src/lib.rs:73-79,103-112),
+ * as the reference's serde does.  Free the committee before its context. */
 typedef struct nt_committee nt_committee;
 int nt_committee_create(nt_ctx *ctx, const nt_keyset *ks, const uint32_t *stake, const uint64_t *worker_first,
                         const uint32_t *worker_ids, uint32_t quorum, nt_committee **out);
@@ -222,7 +256,15 @@ int nt_small_call_model(const nt_ctx *ctx, double *out9);
 void *nt_host_alloc(uint64_t bytes);
 void nt_host_free(void *p);
 
-/* ---- device-resident entry points (enqueue only) ---------------------- */
+/* ---- device-resident entry points (enqueue only) ----------------------
+ * Batches enqueued back to back on two streams overlap only if the two streams
+ * sit on different hardware queues: HIP multiplexes a process's streams over
+ * GPU_MAX_HW_QUEUES (4) queues and may hand two streams the same one, whose
+ * kernels then run strictly in order.  nt_dev_stream returns device entry
+ * `dev`'s two compute streams (which = 0 / 1), created on queues of their own
+ * (a CU-masked stream never shares its queue; the mask enables every CU): a
+ * caller pipelining device-API batches should alternate between them. */
+int nt_dev_stream(nt_ctx *ctx, int dev, int which, void **out);
 int nt_dev_sha512_trunc32(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_data,
                           const uint64_t *d_off, const uint64_t *d_len, uint64_t n,
                           uint8_t *d_out32);

@@ -56,12 +56,7 @@ NT_HD NT_INLINE void ld8(uint32_t w[8], const uint32_t* p) {
 // ---------------------------------------------------------------------------
 constexpr int kWStride = 32;  // words per entry (30 used)
 constexpr int kWChunk = 64;   // consecutive entries built by one thread
-#ifndef NT_BCOMB_BITS
-#define NT_BCOMB_BITS 24
-#endif
-// comb of the base point B (one per device): 24 bits by measurement
-constexpr int kBCombBits = NT_BCOMB_BITS;
-static_assert(kBCombBits == 16 || kBCombBits == 20 || kBCombBits == 22 || kBCombBits == 24 || kBCombBits == 26, "B comb width must be a built width");
+// (the widths of the comb of B, kBCombBits / kBCombFallback: nt_common.hpp)
 
 template <int W>
 struct CombGeom {

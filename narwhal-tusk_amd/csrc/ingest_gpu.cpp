@@ -28,7 +28,7 @@ using namespace ntrt;
 
 struct nt_committee {
   nt_ctx* ctx = nullptr;
-  const nt_keyset* ks = nullptr;
+  std::shared_ptr<KsTables> kt;  // the key set's device tables, kept alive by the committee
   uint32_t nkeys = 0, sbits = 0, quorum = 0;
   struct PerDev {
     int ordinal = -1;
@@ -121,7 +121,7 @@ int nt_committee_create(nt_ctx* ctx, const nt_keyset* ks, const uint32_t* stake,
   const uint32_t nk = ks->nkeys;
   auto cm = std::make_unique<nt_committee>();
   cm->ctx = ctx;
-  cm->ks = ks;
+  cm->kt = ks->t;
   cm->nkeys = nk;
   cm->quorum = quorum;
   // host tables
@@ -178,7 +178,7 @@ int nt_committee_create(nt_ctx* ctx, const nt_keyset* ks, const uint32_t* stake,
     c.stake = (const uint32_t*)(m + o_st);
     c.wfirst = (const uint32_t*)(m + o_wf);
     c.wids = (const uint32_t*)(m + o_wid);
-    c.raw = ks->dev[d].d_enc;
+    c.raw = ks->t->dev[d].d_enc;
     c.nkeys = nk;
     c.sbits = sbits;
     c.quorum = quorum;
@@ -287,11 +287,11 @@ int ingest_back(Device& dv, IngestState& S, Side& sd, int parity, Chunk& ch, con
   NT_CHK0(dv.ensure_stash(parity, nsig));
   void* st = parity ? dv.stash2.p : dv.d[B_STASH].p;
   void* so = parity ? dv.sort2.p : dv.d[B_SORT].p;
-  const auto& kd = cm.ks->dev[dv.group];
+  const auto& kd = cm.kt->dev[dv.group];
   NT_CHK0(dv.keyset_launch(s, st, [&] {
-    return nt::launch_verify_keyset(NT_MODE_MIXED, cm.ks->bits, b.keys, (const uint8_t*)b.sigs, b.mbase, b.smoff,
-                                    b.smlen, nsig, kd.d_meta, kd.d_enc, kd.d_comb, cm.ks->nkeys, dv.d_combB, st, so,
-                                    sd.words.as<uint64_t>(), dv.cus, s);
+    return nt::launch_verify_keyset(NT_MODE_MIXED, cm.kt->bits, b.keys, (const uint8_t*)b.sigs, b.mbase, b.smoff,
+                                    b.smlen, nsig, kd.d_meta, kd.d_enc, kd.d_comb, cm.kt->nkeys, dv.d_combB, dv.bbits,
+                                    st, so, sd.words.as<uint64_t>(), dv.cus, s);
   }));
   NT_TRY(nt::launch_group_and(b.gfirst, b.gcnt, m, b.sig_words, (uint64_t*)b.grp_words, s));
   NT_TRY(nt::launch_cert_verdict(pd.c, b, gc_round, s));
@@ -303,6 +303,7 @@ int ingest_shard(Device& dv, const nt_committee& cm, const uint8_t* data, const 
                  uint64_t lo, uint64_t hi, uint64_t gc_round, uint8_t* out) {
   const uint64_t n = hi - lo;
   if (!n) return NT_OK;
+  NT_CHK0(comb_b_for(dv));
   if (!dv.ingest) {
     auto st = std::make_shared<IngestState>();
     st->ordinal = dv.ordinal;

@@ -1,10 +1,14 @@
-// k_keyset_cofactorless_w20.hip -- key-cache kernels, cofactorless mode, 20-bit key combs
-// (one translation unit per mode and comb width: the build compiles them in parallel).
+// k_keyset_cofactorless_w20.hip -- key-cache kernels, cofactorless mode, 20-bit key combs, for
+// both widths of the comb of B (one translation unit per mode and key-comb width:
+// the build compiles them in parallel).
 #include "k_keyset.inc"
 
+#define NT_KS_INST(WB)                                                                                          \
+  template hipError_t launch_keyset_m<kCofactorless, 20, WB>(                                                          \
+      const KsPlan&, const uint32_t*, const uint8_t*, const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, \
+      const uint32_t*, const uint32_t*, const uint32_t*, uint32_t, const uint32_t*, void*, uint64_t*,            \
+      const uint32_t*, uint8_t*, uint32_t*, hipStream_t);
 namespace nt {
-template hipError_t launch_keyset_m<kCofactorless, 20>(const KsPlan&, const uint32_t*, const uint8_t*, const uint8_t*,
-                                             const uint64_t*, const uint64_t*, uint64_t, const uint32_t*,
-                                             const uint32_t*, const uint32_t*, uint32_t, const uint32_t*,
-                                             void*, uint64_t*, const uint32_t*, uint8_t*, uint32_t*, hipStream_t);
+NT_KS_INST(kBCombBits)
+NT_KS_INST(kBCombFallback)
 }  // namespace nt

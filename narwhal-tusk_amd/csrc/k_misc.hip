@@ -247,6 +247,7 @@ __global__ __launch_bounds__(kBlock) void k_group_and(const uint64_t* __restrict
 // --------------------------------------------------------------------------
 // Keygen + signing (RFC 8032 / dalek Keypair::sign)
 // --------------------------------------------------------------------------
+template <int WB>
 __global__ __launch_bounds__(kBlock) void k_ed25519_sign(const uint32_t* __restrict__ seed,
                                                         const uint8_t* __restrict__ msg,
                                                         const uint64_t* __restrict__ off,
@@ -254,7 +255,7 @@ __global__ __launch_bounds__(kBlock) void k_ed25519_sign(const uint32_t* __restr
                                                         const uint32_t* __restrict__ combB,
                                                         uint32_t* __restrict__ out_pk,
                                                         uint32_t* __restrict__ out_sig) {
-  const BComb wb{combB};
+  const WideComb<WB> wb{combB};
   for (uint64_t base = (uint64_t)blockIdx.x * kBlock; base < n; base += (uint64_t)gridDim.x * kBlock) {
     const uint64_t gi = base + threadIdx.x;
     const uint32_t active = gi < n;
@@ -310,14 +311,20 @@ int keyset_occupancy() { return keyset_occ(); }
 
 hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
                          const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
-                         const uint32_t* d_combB, void* d_ws, uint32_t ws_slots, uint64_t* d_out_words,
+                         const uint32_t* d_combB, int bbits, void* d_ws, uint32_t ws_slots, uint64_t* d_out_words,
                          hipStream_t s) {
   if (n == 0) return hipSuccess;
+  if (!d_combB || !d_ws) return hipErrorInvalidValue;
   const uint64_t blocks = verify_grid(n, ws_slots);
-  return mode == kStrict
-             ? launch_verify_m<kStrict>(blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_combB, d_ws, d_out_words, s)
-             : launch_verify_m<kCofactorless>(blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_combB, d_ws,
-                                              d_out_words, s);
+#define NT_V_ARGS blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_combB, d_ws, d_out_words, s
+  if (bbits == kBCombBits)
+    return mode == kStrict ? launch_verify_m<kStrict, kBCombBits>(NT_V_ARGS)
+                           : launch_verify_m<kCofactorless, kBCombBits>(NT_V_ARGS);
+  if (bbits == kBCombFallback)
+    return mode == kStrict ? launch_verify_m<kStrict, kBCombFallback>(NT_V_ARGS)
+                           : launch_verify_m<kCofactorless, kBCombFallback>(NT_V_ARGS);
+#undef NT_V_ARGS
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_group_and(const uint64_t* d_first, const uint32_t* d_cnt, uint64_t G,
@@ -339,14 +346,19 @@ hipError_t launch_group_msgs(const uint64_t* d_first, const uint32_t* d_cnt, uin
 }
 
 hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, const uint64_t* d_off,
-                       const uint64_t* d_len, uint64_t n, const uint32_t* d_combB, uint8_t* d_pk,
+                       const uint64_t* d_len, uint64_t n, const uint32_t* d_combB, int bbits, uint8_t* d_pk,
                        uint8_t* d_sig, uint32_t max_blocks, hipStream_t s) {
   if (n == 0) return hipSuccess;
+  if (!d_combB) return hipErrorInvalidValue;
   uint64_t blocks = (n + kBlock - 1) / kBlock;
   if (blocks > max_blocks) blocks = max_blocks;
-  hipLaunchKernelGGL(k_ed25519_sign, dim3((uint32_t)blocks), dim3(kBlock), 0, s,
-                     (const uint32_t*)d_seed, d_msg, d_off, d_len, n, d_combB, (uint32_t*)d_pk,
-                     (uint32_t*)d_sig);
+#define NT_SIGN_LAUNCH(WB)                                                                              \
+  hipLaunchKernelGGL(k_ed25519_sign<WB>, dim3((uint32_t)blocks), dim3(kBlock), 0, s,                   \
+                     (const uint32_t*)d_seed, d_msg, d_off, d_len, n, d_combB, (uint32_t*)d_pk, (uint32_t*)d_sig)
+  if (bbits == kBCombBits) NT_SIGN_LAUNCH(kBCombBits);
+  else if (bbits == kBCombFallback) NT_SIGN_LAUNCH(kBCombFallback);
+  else return hipErrorInvalidValue;
+#undef NT_SIGN_LAUNCH
   return hipGetLastError();
 }
 
@@ -380,15 +392,7 @@ hipError_t launch_wcomb_build(int bits, const uint32_t* d_enc, uint32_t nkeys, i
   switch (bits) {
     case kKeyCombWide: return wcomb_build<kKeyCombWide>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
     case kKeyCombMid: return wcomb_build<kKeyCombMid>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
-    case 24: return wcomb_build<24>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);  // B only
-    case 22:  // B only, -DNT_BCOMB_BITS=22 / 26 builds (A/B)
-      if constexpr (kBCombBits == 22)
-        return wcomb_build<22>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
-      return hipErrorInvalidValue;
-    case 26:
-      if constexpr (kBCombBits == 26)
-        return wcomb_build<26>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
-      return hipErrorInvalidValue;
+    case kBCombBits: return wcomb_build<kBCombBits>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);  // B only
     case kKeyCombNarrow:
       return wcomb_build<kKeyCombNarrow>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
     default: return hipErrorInvalidValue;
@@ -541,9 +545,10 @@ KsPlan keyset_plan(uint64_t n, uint32_t cus) {
 hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                                 const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                                 const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
-                                const uint32_t* d_combB, void* d_stash, void* d_sort, uint64_t* d_out_words,
+                                const uint32_t* d_combB, int bbits, void* d_stash, void* d_sort, uint64_t* d_out_words,
                                 uint32_t cus, hipStream_t s) {
-  if (!d_sort || !d_stash) return hipErrorInvalidValue;
+  if (!d_sort || !d_stash || !d_combB) return hipErrorInvalidValue;
+  if (bbits != kBCombBits && bbits != kBCombFallback) return hipErrorInvalidValue;
   uint32_t* ctr = (uint32_t*)d_sort;
   uint32_t* hist = ctr + kSortHdr / 4;
   uint32_t* p = hist + kSortBuckets * kCtrStride;
@@ -574,20 +579,18 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
 #define NT_KS_ARGS                                                                                           \
   pl, d_key_idx + lo, d_sig + 64 * lo, d_msg, d_off + lo, d_len + lo, m, d_meta, d_enc, d_combA, nkeys,     \
       d_combB, d_stash, d_out_words + lo / 64, perm, bytes, ctr, s
-    if (key_bits == kKeyCombWide)
-      e = mode == kStrict   ? launch_keyset_m<kStrict, kKeyCombWide>(NT_KS_ARGS)
-          : mode == kMixed  ? launch_keyset_m<kMixed, kKeyCombWide>(NT_KS_ARGS)
-                            : launch_keyset_m<kCofactorless, kKeyCombWide>(NT_KS_ARGS);
-    else if (key_bits == kKeyCombMid)
-      e = mode == kStrict   ? launch_keyset_m<kStrict, kKeyCombMid>(NT_KS_ARGS)
-          : mode == kMixed  ? launch_keyset_m<kMixed, kKeyCombMid>(NT_KS_ARGS)
-                            : launch_keyset_m<kCofactorless, kKeyCombMid>(NT_KS_ARGS);
-    else if (key_bits == kKeyCombNarrow)
-      e = mode == kStrict   ? launch_keyset_m<kStrict, kKeyCombNarrow>(NT_KS_ARGS)
-          : mode == kMixed  ? launch_keyset_m<kMixed, kKeyCombNarrow>(NT_KS_ARGS)
-                            : launch_keyset_m<kCofactorless, kKeyCombNarrow>(NT_KS_ARGS);
-    else
-      e = hipErrorInvalidValue;
+#define NT_KS_MODES(WA, WB)                                                  \
+  (mode == kStrict  ? launch_keyset_m<kStrict, WA, WB>(NT_KS_ARGS)            \
+   : mode == kMixed ? launch_keyset_m<kMixed, WA, WB>(NT_KS_ARGS)             \
+                    : launch_keyset_m<kCofactorless, WA, WB>(NT_KS_ARGS))
+#define NT_KS_WIDTHS(WB)                                                     \
+  (key_bits == kKeyCombWide     ? NT_KS_MODES(kKeyCombWide, WB)              \
+   : key_bits == kKeyCombMid    ? NT_KS_MODES(kKeyCombMid, WB)               \
+   : key_bits == kKeyCombNarrow ? NT_KS_MODES(kKeyCombNarrow, WB)            \
+                                : hipErrorInvalidValue)
+    e = bbits == kBCombBits ? NT_KS_WIDTHS(kBCombBits) : NT_KS_WIDTHS(kBCombFallback);
+#undef NT_KS_WIDTHS
+#undef NT_KS_MODES
 #undef NT_KS_ARGS
     if (e != hipSuccess) return e;
     if (perm) {
@@ -613,9 +616,7 @@ static size_t comb_size(int bits, int what) {
   return bits == kKeyCombWide     ? comb_size<kKeyCombWide>(what)
          : bits == kKeyCombMid    ? comb_size<kKeyCombMid>(what)
          : bits == kKeyCombNarrow ? comb_size<kKeyCombNarrow>(what)
-         : bits == 24             ? comb_size<24>(what)
-         : bits == 22             ? comb_size<22>(what)
-         : bits == 26             ? comb_size<26>(what)
+         : bits == kBCombBits     ? comb_size<kBCombBits>(what)
                                   : 0;
 }
 size_t wcomb_bytes_per_key(int bits) { return comb_size(bits, 0); }
@@ -623,7 +624,6 @@ size_t wcomb_bases_bytes_per_key(int bits) { return comb_size(bits, 1); }
 size_t wcomb_fill_tmp_bytes_per_key(int bits) { return comb_size(bits, 2); }
 // keys per fill launch: >= 128k threads per launch (16 keys at W = 16, 2 at W = 20)
 uint32_t wcomb_fill_batch(int bits) { return (uint32_t)comb_size(bits, 3); }
-int bcomb_bits() { return kBCombBits; }
 // verify grid: one 512-signature block per workspace slot, at most ws_slots
 uint64_t verify_grid(uint64_t n, uint32_t ws_slots) {
   const uint64_t blocks = (n + kVPer * kBlock - 1) / (kVPer * kBlock);  // kVPer signatures per lane
@@ -645,15 +645,12 @@ uint32_t keyset_per_lane() {
   static const uint32_t m = (uint32_t)env_occ("NT_KEYSET_PER_LANE", kKsPerLane, 1, kKsPerLane);
   return m;
 }
-// stash of a call's launches (each <= kKsMaxPerLaunch signatures): waves x
-// (stash rows of a wave) x 64 lanes x 160 B, the larger of the first launch's
-// and the last (partial) launch's plan
+// stash of any launch of at most n signatures (each <= kKsMaxPerLaunch):
+// ks_stash_rows_bound rows x 64 lanes x 160 B, an upper bound of every plan's
+// waves x stash rows that grows with n (ks_plan.hpp)
 size_t keyset_stash_bytes(uint64_t n, uint32_t cus) {
-  const uint64_t first = n < kKsMaxPerLaunch ? n : kKsMaxPerLaunch;
-  const uint64_t last = n > kKsMaxPerLaunch && n % kKsMaxPerLaunch ? n % kKsMaxPerLaunch : first;
-  const KsPlan a = keyset_plan(first, cus), b = keyset_plan(last, cus);
-  const uint64_t ra = (uint64_t)a.waves * a.stash_rows(), rb = (uint64_t)b.waves * b.stash_rows();
-  return (size_t)((ra > rb ? ra : rb) + 1) * 64 * kKsQuads * 16;
+  const uint64_t m = n < kKsMaxPerLaunch ? n : kKsMaxPerLaunch;
+  return (size_t)ks_stash_rows_bound((m + 63) / 64, cus) * 64 * kKsQuads * 16;
 }
 size_t ws_bytes_per_slot() { return (size_t)kAEntries * kAQuads * kBlock * 16; }
 

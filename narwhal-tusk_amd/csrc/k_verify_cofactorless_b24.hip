@@ -1,0 +1,9 @@
+// k_verify_cofactorless_b24.hip -- verify kernels, cofactorless mode, 24-bit comb of B (one translation
+// unit per mode and comb width, so the build compiles them in parallel).
+#include "k_verify.inc"
+
+namespace nt {
+template hipError_t launch_verify_m<kCofactorless, 24>(uint64_t, const uint8_t*, const uint8_t*, const uint8_t*,
+                                              const uint64_t*, const uint64_t*, uint64_t, const uint32_t*, void*,
+                                              uint64_t*, hipStream_t);
+}  // namespace nt

@@ -55,7 +55,6 @@ struct WideComb {
     }
   }
 };
-using BComb = WideComb<kBCombBits>;
 
 // Per-lane point tables in the global workspace, uint4 granules.  Lane-major
 // ([slot][lane][entry][quad], NT_ATAB_LANE_MAJOR=1): an entry is 160 contiguous
@@ -204,11 +203,13 @@ struct KsStash {
 // k_keyset_<mode>.hip (one translation unit per kernel family and mode, so
 // the build compiles them in parallel); dispatched by launch_verify /
 // launch_verify_keyset in k_misc.hip.
-template <int MODE>
+// WB = digit width of the comb of B (kBCombBits or kBCombFallback), WA = the
+// committee keys' comb width.
+template <int MODE, int WB>
 hipError_t launch_verify_m(uint64_t blocks, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
                            const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_combB,
                            void* d_ws, uint64_t* d_out_words, hipStream_t s);
-template <int MODE, int WA>
+template <int MODE, int WA, int WB>
 hipError_t launch_keyset_m(const KsPlan& plan, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                            const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                            const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,

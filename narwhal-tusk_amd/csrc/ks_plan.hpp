@@ -71,6 +71,17 @@ inline KsPlan ks_stream_plan(uint64_t n, uint32_t cus, uint32_t cap, int force_p
   return p;
 }
 
+// Stash rows (waves x rows per wave) any plan of either kind needs for a launch
+// of at most `rows` rows: streamed, W (ceil(rows / W) + 2) <= rows + 3 W;
+// chunked, W (base + 1) <= rows + W, with W <= 3 x 4 x cus resident waves.
+// Monotone in rows, so a caller that sizes the stash once for its largest
+// launch may run every smaller one into it (the chunked plan's own
+// waves x stash_rows is NOT monotone -- 36,864 rows on 256 CUs plan 18,432
+// stash rows, 30,720 rows plan 30,720).
+inline uint64_t ks_stash_rows_bound(uint64_t rows, uint32_t cus) {
+  return rows + 3ull * 3 * 4 * (cus ? cus : 1) + 1;
+}
+
 // force_per_simd: 0 = cheaper of 2 and 3, else 2 or 3; cap: most rows per chunk (1..64)
 inline KsPlan ks_plan(uint64_t n, uint32_t cus, uint32_t cap, int force_per_simd) {
   const double A = 16.66, B = 15.07, kLone = 1.07;

@@ -35,4 +35,12 @@ constexpr int kKeyCombWide = 20;    // 13 additions per [k]A, 872 MB per key: us
 constexpr int kKeyCombMid = 18;     // 15 additions, 252 MB per key (NT_KEYSET_COMB_BITS=18, A/B)
 constexpr int kKeyCombNarrow = 16;  // 16 additions, 67 MB per key
 
+// Digit widths of the comb of the base point B (one per device ordinal): 24 bits
+// by measurement, 20 bits when the context's HBM budget or the
+// device's free memory cannot hold 11.8 GB (ntcrypto.cpp: comb_b_for).  Every
+// kernel that reads it is compiled for both; the launchers dispatch on the width
+// of the comb the device entry holds.
+constexpr int kBCombBits = 24;      // 11 additions per [s]B, 11.8 GB (the host harness builds this one)
+constexpr int kBCombFallback = 20;  // 13 additions, 872 MB
+
 }  // namespace nt

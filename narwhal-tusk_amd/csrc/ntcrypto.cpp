@@ -1,9 +1,10 @@
 // ntcrypto.cpp -- host side of the C ABI (include/ntcrypto.h).
 //
 // Owns one `Device` per GPU (per entry of nt_init_devices: a repeated ordinal
-// gets its own): non-blocking HIP streams, the wide comb of B (24-bit digits,
-// 11.8 GB per Device; 872 MB in a -DNT_BCOMB_BITS=20 build), the per-lane [k]A
-// table workspace and grow-only device/pinned staging buffers.
+// gets its own): non-blocking HIP streams and grow-only device/pinned staging;
+// on the first call that needs them, the wide comb of B (24-bit digits, 11.8 GB,
+// shared per device ordinal; 20-bit, 872 MB, under an HBM budget or when the
+// device cannot hold the wide one) and the per-lane [k]A table workspace.
 // Host entry points shard items over devices by contiguous index ranges (one
 // host thread per device), stage through pinned memory, launch, and gather the
 // bitmaps / digests.  There is deliberately no CPU compute path: if HIP or the
@@ -41,26 +42,97 @@ bool is_pinned(const void* p, uint64_t bytes) {
   return (uintptr_t)p + bytes <= it->first + it->second;
 }
 
-// comb of B per device ordinal, shared across device entries and contexts
+// comb of B per (device ordinal, digit width), shared across device entries and contexts
 std::mutex g_combb_mu;
-std::map<int, std::weak_ptr<CombB>> g_combb;
+std::map<std::pair<int, int>, std::weak_ptr<CombB>> g_combb;
 
-std::shared_ptr<CombB> shared_comb_b(Device& dv, int& rc) {
+std::shared_ptr<CombB> shared_comb_b(Device& dv, int bits, int& rc) {
   static const uint32_t kB[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                                  0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};  // encoding of B
   std::lock_guard<std::mutex> lk(g_combb_mu);
-  if (auto c = g_combb[dv.ordinal].lock()) return c;
+  if (auto c = g_combb[{dv.ordinal, bits}].lock()) return c;
   auto c = std::make_shared<CombB>();
   c->ordinal = dv.ordinal;
-  if (hipMalloc(&c->p, nt::wcomb_bytes_per_key(nt::bcomb_bits())) != hipSuccess) {
+  c->bits = bits;
+  if (hipSetDevice(dv.ordinal) != hipSuccess) {
+    rc = NT_EHIP;
+    return nullptr;
+  }
+  if (hipMalloc(&c->p, nt::wcomb_bytes_per_key(bits)) != hipSuccess) {
+    (void)hipGetLastError();  // an out-of-memory hipMalloc leaves no sticky error: clear it
     c->p = nullptr;
     rc = NT_ENOMEM;
     return nullptr;
   }
-  rc = dv.build_wcombs(nt::bcomb_bits(), kB, 1, 0, c->p, nullptr);
+  rc = dv.build_wcombs(bits, kB, 1, 0, c->p, nullptr);
   if (rc != NT_OK) return nullptr;
-  g_combb[dv.ordinal] = c;
+  g_combb[{dv.ordinal, bits}] = c;
   return c;
+}
+
+// NT_BCOMB_BITS=24|20 forces the width of the comb of B (A/B runs, tests)
+static int forced_bcomb_bits() {
+  const char* e = std::getenv("NT_BCOMB_BITS");
+  const int b = e ? std::atoi(e) : 0;
+  return b == nt::kBCombBits || b == nt::kBCombFallback ? b : 0;
+}
+
+// HBM the device must keep free beside a 24-bit comb of B (two slots' verify
+// workspaces + staging); below it the entry takes the 20-bit comb
+constexpr uint64_t kCombHeadroom = 4ull << 30;
+
+// The comb of B of execution slot dv: its entry's, created on first use.  The
+// entry picks the widest width that (a) fits the context's HBM budget on the
+// entry, (b) leaves kCombHeadroom of the device free and (c) hipMalloc grants:
+// 24-bit digits (11 additions per [s]B, 11.8 GB), else 20-bit (13, 872 MB).
+int comb_b_for(Device& dv) {
+  if (dv.d_combB) return NT_OK;
+  Device& e = *dv.entry;
+  std::lock_guard<std::mutex> lk(e.tables_mu);
+  if (!e.combB) {
+    const int forced = forced_bcomb_bits();
+    int rc = NT_ENOMEM;
+    for (const int w : {nt::kBCombBits, nt::kBCombFallback}) {
+      if (forced && w != forced) continue;
+      const uint64_t bytes = nt::wcomb_bytes_per_key(w);
+      if (!forced && w == nt::kBCombBits) {
+        size_t fr = 0, tot = 0;
+        if (hipSetDevice(e.ordinal) != hipSuccess || hipMemGetInfo(&fr, &tot) != hipSuccess) return NT_EHIP;
+        // an existing comb of this width on the ordinal costs nothing more
+        std::shared_ptr<CombB> have;
+        {
+          std::lock_guard<std::mutex> g(g_combb_mu);
+          auto it = g_combb.find({e.ordinal, w});
+          if (it != g_combb.end()) have = it->second.lock();
+        }
+        if (!have && fr < bytes + kCombHeadroom) continue;
+      }
+      if (!e.budget->reserve(bytes)) continue;
+      auto c = shared_comb_b(e, w, rc);
+      if (!c) {
+        e.budget->release(bytes);
+        if (rc != NT_ENOMEM) return rc;
+        continue;
+      }
+      e.combB = c;
+      e.d_combB = c->p;
+      e.bbits = w;
+      e.comb_reserved = bytes;
+      rc = NT_OK;
+      break;
+    }
+    if (rc != NT_OK) return rc;
+  }
+  dv.combB = e.combB;
+  dv.d_combB = e.d_combB;
+  dv.bbits = e.bbits;
+  return NT_OK;
+}
+
+// everything the verify kernel of slot dv reads besides its inputs
+int verify_tables(Device& dv) {
+  NT_CHK(comb_b_for(dv));
+  return dv.ensure_ws();
 }
 
 }  // namespace ntrt
@@ -103,16 +175,31 @@ static long env_slots() {
   return e && *e ? std::atol(e) : 2;
 }
 
+// NT_HBM_BUDGET: bytes of tables per device entry, with an optional K / M / G suffix (0 / unset = no cap)
+static uint64_t env_budget() {
+  const char* e = std::getenv("NT_HBM_BUDGET");
+  if (!e || !*e) return 0;
+  char* end = nullptr;
+  const double v = std::strtod(e, &end);
+  double mul = 1;
+  if (end && (*end == 'k' || *end == 'K')) mul = 1024.0;
+  if (end && (*end == 'm' || *end == 'M')) mul = 1024.0 * 1024;
+  if (end && (*end == 'g' || *end == 'G')) mul = 1024.0 * 1024 * 1024;
+  return v > 0 ? (uint64_t)(v * mul) : 0;
+}
+
 static int init_common(nt_ctx** out, const std::vector<int>& ords) {
   if (!out) return NT_EINVAL;
   *out = nullptr;
   auto ctx = std::make_unique<nt_ctx>();
   ctx->small_model = with_env(NtSmallModel{});
+  ctx->hbm_budget = env_budget();
   const int slots = std::max(1, std::min(8, (int)env_slots()));
   for (int o : ords) {
     auto d = std::make_unique<Device>();
     int rc = d->init(o, (int)ctx->devs.size());
     if (rc != NT_OK) return rc;
+    d->budget->limit = ctx->hbm_budget;
     for (int k = 1; k < slots; ++k) {
       auto x = std::make_unique<Device>();
       rc = x->init(o, (int)ctx->devs.size(), d.get());
@@ -156,6 +243,56 @@ int nt_init_devices(nt_ctx** out, const int* ordinals, int n) {
 void nt_free(nt_ctx* ctx) { delete ctx; }
 
 int nt_num_devices(const nt_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+int nt_set_hbm_budget(nt_ctx* ctx, uint64_t bytes_per_device) {
+  if (!ctx) return NT_EINVAL;
+  ctx->hbm_budget = bytes_per_device;
+  for (auto& d : ctx->devs) {
+    std::lock_guard<std::mutex> lk(d->budget->mu);
+    d->budget->limit = bytes_per_device;
+  }
+  return NT_OK;
+}
+
+int nt_memory_info(nt_ctx* ctx, int dev, uint64_t* out8) {
+  if (!ctx || !out8 || dev < 0 || dev >= (int)ctx->devs.size()) return NT_EINVAL;
+  Device& e = *ctx->devs[dev];
+  uint64_t ws = 0, stash = 0, staging = 0;
+  std::vector<Device*> slots{&e};
+  for (auto& x : e.extra) slots.push_back(x.get());
+  for (Device* sl : slots) {
+    std::lock_guard<std::mutex> lk(sl->mu);
+    ws += (sl->d_ws ? nt::ws_bytes_per_slot() * sl->ws_slots : 0) + sl->ws2.cap;
+    stash += sl->d[B_STASH].cap + sl->d[B_SORT].cap + sl->stash2.cap + sl->sort2.cap;
+    for (int b = 0; b < B_NBUF; ++b)
+      if (b != B_STASH && b != B_SORT) staging += sl->d[b].cap;
+  }
+  uint64_t comb_bits = 0, comb_bytes = 0, reserved = 0;
+  {
+    std::lock_guard<std::mutex> lk(e.tables_mu);
+    if (e.combB) {
+      comb_bits = (uint64_t)e.bbits;
+      comb_bytes = nt::wcomb_bytes_per_key(e.bbits);
+    }
+    reserved = e.comb_reserved;
+  }
+  uint64_t limit = 0, held = 0;
+  {
+    std::lock_guard<std::mutex> lk(e.budget->mu);
+    limit = e.budget->limit;
+    held = e.budget->held;
+  }
+  const uint64_t v[8] = {comb_bits, comb_bytes, held - std::min(held, reserved), ws, stash, staging, limit, held};
+  std::memcpy(out8, v, sizeof v);
+  return NT_OK;
+}
+
+int nt_dev_stream(nt_ctx* ctx, int dev, int which, void** out) {
+  if (!ctx || !out || dev < 0 || dev >= (int)ctx->devs.size() || (which != 0 && which != 1)) return NT_EINVAL;
+  Device& d = *ctx->devs[dev];
+  *out = (void*)(which ? d.stream2 : d.stream);
+  return NT_OK;
+}
 
 int nt_set_small_call_path(nt_ctx* ctx, int mode, int threads) {
   if (!ctx || mode < NT_SMALL_OFF || mode > NT_SMALL_ALWAYS) return NT_EINVAL;
@@ -543,6 +680,7 @@ int nt_ed25519_verify_strict(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* si
   }
   ctx->calls_gpu++;
   return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
+    NT_CHK(verify_tables(dv));
     const uint64_t m = hi - lo, words = (m + 63) / 64;
     const auto ch = plan_chunks(m, pipe_round(nt::verify_round_sigs(dv.cus)));
     MsgStage ms;
@@ -631,6 +769,7 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
   if (out_sig_bitmap) std::memset(out_sig_bitmap, 0, (nsig_total + 7) / 8);
   std::mutex sig_mu;
   return run_sharded(ctx, G, 64, [&](Device& dv, uint64_t glo, uint64_t ghi) -> int {
+    NT_CHK(ks ? comb_b_for(dv) : verify_tables(dv));
     const uint64_t gm = ghi - glo;
     uint64_t m = 0;
     for (uint64_t g = glo; g < ghi; ++g) m += cnt[g];
@@ -672,7 +811,7 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
       for (size_t c = 0; c < C; ++c) mc = std::max(mc, E[c + 1] - E[c]);
       NT_CHK(dv.ensure_stash(0, mc));
       if (C > 1) NT_CHK(dv.ensure_stash(1, mc));
-      pd_meta = &ks->dev[dev_index(ctx, dv)];
+      pd_meta = &ks->t->dev[dev_index(ctx, dv)];
     }
     uint8_t* hkey = dv.h[B_PK].as<uint8_t>();
     uint8_t* hsig = dv.h[B_SIG].as<uint8_t>();
@@ -707,12 +846,13 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
         NT_TRY(nt::launch_group_msgs(dv.d[B_FIRST].as<uint64_t>() + gl, dv.d[B_CNT].as<uint32_t>() + gl, g1 - g0,
                                      (uint64_t*)doff, (uint64_t*)dlen, s));
         if (ks) {
-          const auto& pd = *(const nt_keyset::PerDev*)pd_meta;
+          const auto& pd = *(const KsTables::PerDev*)pd_meta;
           void* st = (c & 1) ? dv.stash2.p : dv.d[B_STASH].p;
           void* so = (c & 1) ? dv.sort2.p : dv.d[B_SORT].p;
           NT_CHK(dv.keyset_launch(s, st, [&] {
             return nt::launch_verify_keyset(NT_MODE_COFACTORLESS, ks->bits, (const uint32_t*)dk, dsig, dmsg, doff, dlen,
-                                            mc, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, st, so, dout, dv.cus, s);
+                                            mc, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, dv.bbits, st, so,
+                                            dout, dv.cus, s);
           }));
         } else {
           NT_CHK(dv.verify_chunk((int)c, NT_MODE_COFACTORLESS, dk, dsig, dmsg, doff, dlen, mc, dout));
@@ -776,6 +916,7 @@ int nt_ed25519_sign_batch(nt_ctx* ctx, const uint8_t* seed32, const uint8_t* msg
   if (sig64 && n && (!off || !len)) return NT_EINVAL;
   if (n == 0) return NT_OK;
   return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
+    NT_CHK(comb_b_for(dv));
     const uint64_t m = hi - lo;
     const uint8_t* d_msg = nullptr;
     const uint64_t *d_off = nullptr, *d_len = nullptr;
@@ -790,7 +931,7 @@ int nt_ed25519_sign_batch(nt_ctx* ctx, const uint8_t* seed32, const uint8_t* msg
     NT_CHK(dv.d[B_SIG].ensure(m * 64));
     NT_CHK(dv.d[B_OUT].ensure(m * 32));
     NT_TRY(hipMemcpyAsync(dv.d[B_OUT].p, seed32 + 32 * lo, m * 32, hipMemcpyHostToDevice, dv.stream));
-    NT_TRY(nt::launch_sign(dv.d[B_OUT].as<uint8_t>(), d_msg, d_off, d_len, m, dv.d_combB,
+    NT_TRY(nt::launch_sign(dv.d[B_OUT].as<uint8_t>(), d_msg, d_off, d_len, m, dv.d_combB, dv.bbits,
                            dv.d[B_PK].as<uint8_t>(), sig64 ? dv.d[B_SIG].as<uint8_t>() : nullptr,
                            dv.sign_blocks, dv.stream));
     NT_TRY(hipMemcpyAsync(pk32 + 32 * lo, dv.d[B_PK].p, m * 32, hipMemcpyDeviceToHost, dv.stream));
@@ -806,23 +947,36 @@ int nt_ed25519_keypair_batch(nt_ctx* ctx, const uint8_t* seed32, uint64_t n, uin
 }
 
 // ---- committee key cache --------------------------------------------------
-// Comb width of a new key set: 20-bit combs (13 additions per [k]A, 872 MB per
-// key) when every device can hold them and keep 1/8 of its HBM free, else
-// 16-bit combs (16 additions, 67 MB per key).  NT_KEYSET_COMB_BITS=16|18|20 forces
-// one (18 bits: 15 additions, 252 MB per key).
+// Comb width of a new key set: the widest of 20 / 18 / 16-bit digits (13 / 15 /
+// 16 additions per [k]A; 872 / 252 / 67 MB per key) that, on every device entry
+// of the context, fits the context's HBM budget beside the comb of B and the
+// tables the entry already holds, and leaves 1/8 of the device's HBM free.
+// With no width passing the free-memory test the 16-bit combs are tried anyway
+// (hipMalloc decides); 0 = not even those fit the budget.
+// NT_KEYSET_COMB_BITS=16|18|20 forces one (18 bits: the A/B width of round 2).
 static int keyset_comb_bits(nt_ctx* ctx, uint32_t nkeys) {
   if (const char* e = std::getenv("NT_KEYSET_COMB_BITS")) {
     const int b = std::atoi(e);
     if (b == nt::kKeyCombWide || b == nt::kKeyCombMid || b == nt::kKeyCombNarrow) return b;
   }
-  const size_t need = nt::wcomb_bytes_per_key(nt::kKeyCombWide) * std::max<uint32_t>(nkeys, 1) +
-                      nt::wcomb_fill_tmp_bytes_per_key(nt::kKeyCombWide) * nt::wcomb_fill_batch(nt::kKeyCombWide);
-  for (auto& d : ctx->devs) {
-    size_t fr = 0, tot = 0;
-    if (hipSetDevice(d->ordinal) != hipSuccess || hipMemGetInfo(&fr, &tot) != hipSuccess) return nt::kKeyCombNarrow;
-    if (fr < need + tot / 8) return nt::kKeyCombNarrow;
+  const uint64_t nk = std::max<uint32_t>(nkeys, 1);
+  for (const int w : {nt::kKeyCombWide, nt::kKeyCombMid, nt::kKeyCombNarrow}) {
+    const uint64_t comb = nt::wcomb_bytes_per_key(w) * nk;
+    const uint64_t need = comb + nt::wcomb_fill_tmp_bytes_per_key(w) * nt::wcomb_fill_batch(w);
+    bool ok = true;
+    for (auto& d : ctx->devs) {
+      size_t fr = 0, tot = 0;
+      if (!d->budget->fits(comb) || hipSetDevice(d->ordinal) != hipSuccess ||
+          hipMemGetInfo(&fr, &tot) != hipSuccess || fr < need + tot / 8) {
+        ok = false;
+        break;
+      }
+    }
+    if (ok) return w;
   }
-  return nt::kKeyCombWide;
+  for (auto& d : ctx->devs)
+    if (!d->budget->fits(nt::wcomb_bytes_per_key(nt::kKeyCombNarrow) * nk)) return 0;
+  return nt::kKeyCombNarrow;
 }
 
 // Small-call path: key encoding and check mode of one key-cache entry, as
@@ -842,23 +996,42 @@ static int keyset_key(const nt_keyset* ks, int mode, uint32_t kraw, uint8_t A[32
 int nt_keyset_create(nt_ctx* ctx, const uint8_t* pk32, uint32_t nkeys, nt_keyset** out) {
   if (!ctx || !out || (nkeys && !pk32)) return NT_EINVAL;
   *out = nullptr;
+  // verification against the set reads the comb of B: it takes its share of the
+  // budget first, the key combs get what is left
+  for (auto& d : ctx->devs) {
+    std::lock_guard<std::mutex> lk(d->mu);
+    NT_CHK(comb_b_for(*d));
+  }
   auto ks = std::make_unique<nt_keyset>();
   ks->ctx = ctx;
   ks->nkeys = nkeys;
   ks->bits = keyset_comb_bits(ctx, nkeys);
+  if (ks->bits == 0) return NT_ENOMEM;
   ks->flags.assign(nkeys, 0);
   if (nkeys) ks->enc.assign(pk32, pk32 + 32ull * nkeys);
-  ks->dev.resize(ctx->devs.size());
+  ks->t = std::make_shared<KsTables>();
+  KsTables& T = *ks->t;
+  T.nkeys = nkeys;
+  T.bits = ks->bits;
+  T.dev.resize(ctx->devs.size());
   for (size_t di = 0; di < ctx->devs.size(); ++di) {
     Device& dv = *ctx->devs[di];
     std::lock_guard<std::mutex> lk(dv.mu);
     NT_TRY(hipSetDevice(dv.ordinal));
-    auto& pd = ks->dev[di];
+    auto& pd = T.dev[di];
     pd.ordinal = dv.ordinal;
     const size_t nk = std::max<uint32_t>(nkeys, 1);
+    const uint64_t comb = nt::wcomb_bytes_per_key(ks->bits) * nk;
+    if (!dv.budget->reserve(comb)) return NT_ENOMEM;
+    pd.budget = dv.budget;
+    pd.reserved = comb;
     if (hipMalloc(&pd.d_enc, 32 * nk) != hipSuccess) return NT_ENOMEM;
     if (hipMalloc(&pd.d_meta, 4 * nk) != hipSuccess) return NT_ENOMEM;
-    if (hipMalloc(&pd.d_comb, nt::wcomb_bytes_per_key(ks->bits) * nk) != hipSuccess) return NT_ENOMEM;
+    if (hipMalloc(&pd.d_comb, comb) != hipSuccess) {
+      (void)hipGetLastError();
+      pd.d_comb = nullptr;
+      return NT_ENOMEM;
+    }
     if (nkeys) {
       NT_TRY(hipMemcpyAsync(pd.d_enc, pk32, 32ull * nkeys, hipMemcpyHostToDevice, dv.stream));
       NT_TRY(hipStreamSynchronize(dv.stream));
@@ -910,7 +1083,8 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
   }
   ctx->calls_gpu++;
   return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
-    const auto& pd = ks->dev[dev_index(ctx, dv)];
+    NT_CHK(comb_b_for(dv));
+    const auto& pd = ks->t->dev[dev_index(ctx, dv)];
     const uint64_t m = hi - lo, words = (m + 63) / 64;
     const auto ch = plan_chunks(m, pipe_round(nt::keyset_round_sigs(dv.cus)));
     MsgStage ms;
@@ -938,7 +1112,7 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
         return nt::launch_verify_keyset(mode, ks->bits, dv.d[B_PK].as<uint32_t>() + a,
                                         dv.d[B_SIG].as<uint8_t>() + 64 * a, dv.d[B_DATA].as<uint8_t>(),
                                         dv.d[B_OFF].as<uint64_t>() + a, dv.d[B_LEN].as<uint64_t>() + a, b - a,
-                                        pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, st, so,
+                                        pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, dv.bbits, st, so,
                                         dv.d[B_OUT].as<uint64_t>() + a / 64, dv.cus, s);
       }));
     }
@@ -990,6 +1164,7 @@ int nt_dev_ed25519_verify(nt_ctx* ctx, int dev, void* stream, int mode, const ui
   hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
   // the [k]A workspaces are per device: launches that use one are ordered by its event
   std::lock_guard<std::mutex> lk(dv->mu);
+  NT_CHK(verify_tables(*dv));
   NT_TRY(dv->verify_dev(mode, d_pk32, d_sig64, d_msg, d_off, d_len, n, d_out_words, s));
   return NT_OK;
 }
@@ -1014,19 +1189,20 @@ int nt_dev_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int dev, void
     return NT_EINVAL;
   NT_TRY(hipSetDevice(dv->ordinal));
   hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
-  const auto& pd = ks->dev[dev];
+  const auto& pd = ks->t->dev[dev];
   // the device's two stashes, shared with the host entry points, each ordered
   // against every other user by its event whatever the streams; successive
   // device-API calls alternate between them (like nt_dev_ed25519_verify's
   // workspaces), so batches on two streams can overlap
   std::lock_guard<std::mutex> lk(dv->mu);
+  NT_CHK(comb_b_for(*dv));
   const int k = (int)(dv->ks_calls++ & 1u);
   NT_CHK(dv->ensure_stash(k, n));
   void* stash = k ? dv->stash2.p : dv->d[B_STASH].p;
   void* so = k ? dv->sort2.p : dv->d[B_SORT].p;
   return dv->keyset_launch(s, stash, [&] {
     return nt::launch_verify_keyset(mode, ks->bits, d_key_idx, d_sig64, d_msg, d_off, d_len, n, pd.d_meta, pd.d_enc,
-                                    pd.d_comb, ks->nkeys, dv->d_combB, stash, so, d_out_words, dv->cus, s);
+                                    pd.d_comb, ks->nkeys, dv->d_combB, dv->bbits, stash, so, d_out_words, dv->cus, s);
   });
 }
 
@@ -1037,7 +1213,9 @@ int nt_dev_ed25519_sign(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_see
   if (!dv) return NT_EINVAL;
   NT_TRY(hipSetDevice(dv->ordinal));
   hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
-  NT_TRY(nt::launch_sign(d_seed32, d_msg, d_off, d_len, n, dv->d_combB, d_pk32, d_sig64,
+  std::lock_guard<std::mutex> lk(dv->mu);
+  NT_CHK(comb_b_for(*dv));
+  NT_TRY(nt::launch_sign(d_seed32, d_msg, d_off, d_len, n, dv->d_combB, dv->bbits, d_pk32, d_sig64,
                          dv->sign_blocks, s));
   return NT_OK;
 }

@@ -3,6 +3,7 @@
 // ingest_gpu.cpp: wire ingestion on the device).  Not part of the ABI.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <atomic>
@@ -76,13 +77,16 @@ bool is_pinned(const void* p, uint64_t bytes);
 
 enum { B_DATA, B_OFF, B_LEN, B_PK, B_SIG, B_OUT, B_OUT2, B_FIRST, B_CNT, B_STASH, B_SORT, B_NBUF };
 
-// The wide comb of B on one device ordinal, shared by every device entry of
-// every context of the process that runs on that ordinal (11.8 GB at 24-bit
-// digits: round 2 paid it per entry -- repeated ordinals, a second Backend, the
-// contention probe's contexts).  Built by the first user, freed
-// with the last (ntcrypto.cpp: shared_comb_b).
+// The wide comb of B of one digit width on one device ordinal, shared by every
+// device entry of every context of the process that runs on that ordinal at
+// that width (11.8 GB at 24-bit digits, 872 MB at 20: round 2 paid it per entry
+// -- repeated ordinals, a second Backend, the contention probe's contexts;
+// ADVICE r02).  Built by the first verify / sign call that needs it (never at
+// nt_init: a digest-only worker pays nothing), freed with the last user
+// (ntcrypto.cpp: shared_comb_b, comb_b_for).
 struct CombB {
   int ordinal = -1;
+  int bits = 0;
   uint32_t* p = nullptr;
   ~CombB() {
     if (!p) return;
@@ -91,15 +95,64 @@ struct CombB {
   }
 };
 struct Device;
-std::shared_ptr<CombB> shared_comb_b(Device& dv, int& rc);
+std::shared_ptr<CombB> shared_comb_b(Device& dv, int bits, int& rc);
+// the comb of B of a slot (created by its entry on first use; ntcrypto.cpp)
+int comb_b_for(Device& dv);
+
+// The context's HBM budget on one device entry (shared by its execution slots
+// and by the key sets built on it): the TABLES whose width degrades to fit --
+// the comb of B (24 -> 20 bits) and the committee key combs (20 -> 18 -> 16) --
+// are reserved against `limit` (NT_HBM_BUDGET / nt_set_hbm_budget; 0 = no cap,
+// only the device's free memory decides).  Workspaces, stashes and staging are
+// per-call and not budgeted (nt_memory_info reports them).
+struct Budget {
+  std::mutex mu;
+  uint64_t limit = 0;
+  uint64_t held = 0;
+  bool reserve(uint64_t b) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (limit && held + b > limit) return false;
+    held += b;
+    return true;
+  }
+  void release(uint64_t b) {
+    std::lock_guard<std::mutex> lk(mu);
+    held -= std::min(held, b);
+  }
+  bool fits(uint64_t b) {
+    std::lock_guard<std::mutex> lk(mu);
+    return !limit || held + b <= limit;
+  }
+};
+
+// A compute stream with a hardware queue of its own.  HIP multiplexes a
+// process's streams over GPU_MAX_HW_QUEUES (4) queues of each priority and,
+// once they exist, hands a new stream the least-used one, so two streams can
+// share a queue -- and kernels of one queue run back to back: measured
+// (rocprofv3 kernel trace, profiles/r04/): the bench's two config-3 streams
+// both landed on one queue and consecutive key-cache launches never
+// overlapped.  A stream created with a CU mask is never given a shared queue;
+// the mask here enables every CU.  NT_SHARED_QUEUES=1 restores plain streams.
+inline hipError_t compute_stream(hipStream_t* s, uint32_t cus) {
+  const char* e = std::getenv("NT_SHARED_QUEUES");
+  if (e && *e == '1') return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  std::vector<uint32_t> mask((cus + 31) / 32, 0xffffffffu);
+  if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+  return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+}
 
 struct Device {
   int ordinal = -1;
   int group = -1;               // index of this device entry in nt_ctx::devs (keyset tables)
-  std::shared_ptr<CombB> combB;  // holds d_combB (shared per ordinal, see CombB)
+  Device* entry = this;         // the device entry this execution slot belongs to
+  std::shared_ptr<Budget> budget;  // the entry's (shared with its slots)
+  std::mutex tables_mu;         // (entry) lazy creation of the comb of B
+  std::shared_ptr<CombB> combB;  // holds d_combB (shared per ordinal and width, see CombB); null until first needed
+  uint64_t comb_reserved = 0;   // (entry) bytes of the comb of B reserved in the budget
   hipStream_t stream = nullptr;
-  uint32_t* d_combB = nullptr;  // wide comb of B (verify, key-cache verify, sign)
-  void* d_ws = nullptr;
+  uint32_t* d_combB = nullptr;  // wide comb of B (verify, key-cache verify, sign): comb_b_for() sets it
+  int bbits = 0;                // its digit width (nt::kBCombBits or nt::kBCombFallback)
+  void* d_ws = nullptr;         // verify workspace: ensure_ws() on the first verify
   uint32_t ws_slots = 0;
   uint32_t sign_blocks = 0;
   uint32_t cus = 0;
@@ -131,6 +184,7 @@ struct Device {
   std::shared_ptr<void> ingest;
 
   ~Device() {
+    if (comb_reserved && budget) budget->release(comb_reserved);
     if (ordinal < 0) return;
     (void)hipSetDevice(ordinal);
     if (stream) (void)hipStreamSynchronize(stream);
@@ -157,9 +211,11 @@ struct Device {
     if (stream) (void)hipStreamDestroy(stream);
   }
 
-  int init(int ord, int grp, const Device* share = nullptr) {
+  int init(int ord, int grp, Device* share = nullptr) {
     ordinal = ord;
     group = grp;
+    entry = share ? share : this;
+    budget = share ? share->budget : std::make_shared<Budget>();
     NT_TRY(hipSetDevice(ord));
     hipDeviceProp_t prop;
     NT_TRY(hipGetDeviceProperties(&prop, ord));
@@ -175,9 +231,10 @@ struct Device {
       NT_TRY(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
       cstream = stream2 = stream;
     } else {
-      NT_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+      // the two compute streams on hardware queues of their own (compute_stream)
+      NT_TRY(compute_stream(&stream, (uint32_t)prop.multiProcessorCount));
       NT_TRY(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
-      NT_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+      NT_TRY(compute_stream(&stream2, (uint32_t)prop.multiProcessorCount));
     }
     NT_TRY(hipEventCreateWithFlags(&ws_done, hipEventDisableTiming));
     NT_TRY(hipEventCreateWithFlags(&stash_done, hipEventDisableTiming));
@@ -185,15 +242,8 @@ struct Device {
     NT_TRY(hipEventCreateWithFlags(&join2, hipEventDisableTiming));
     NT_TRY(hipEventCreateWithFlags(&ws2_done, hipEventDisableTiming));
     NT_TRY(hipEventCreateWithFlags(&stash2_done, hipEventDisableTiming));
-    if (share) {
-      combB = share->combB;
-      d_combB = share->d_combB;
-    } else {
-      int rc = NT_OK;
-      combB = shared_comb_b(*this, rc);
-      if (!combB) return rc;
-      d_combB = combB->p;
-    }
+    // Nothing large is allocated here: the comb of B and the verify workspace
+    // come with the first call that needs them (comb_b_for, ensure_ws).
     // Workspace slots = grid cap of the verify kernel.  Four times the resident
     // workgroups (256-thread blocks, `occupancy` waves per SIMD, 4 SIMDs per CU):
     // up to 2M signatures per launch the grid is then one 512-signature block per
@@ -204,7 +254,6 @@ struct Device {
     ws_slots = slots;
     sign_blocks = (uint32_t)prop.multiProcessorCount * 8;
     cus = (uint32_t)prop.multiProcessorCount;
-    if (hipMalloc(&d_ws, nt::ws_bytes_per_slot() * ws_slots) != hipSuccess) return NT_ENOMEM;
     NT_TRY(hipEventRecord(ws_done, stream));
     NT_TRY(hipEventRecord(stash_done, stream));
     NT_TRY(hipEventRecord(ws2_done, stream));
@@ -236,6 +285,18 @@ struct Device {
     return rc;
   }
 
+  // the [k]A workspace of the verify kernel (ws_slots x 737 KB, ~1.5 GB at
+  // 2,048 slots), on the slot's first verify
+  int ensure_ws() {
+    if (d_ws) return NT_OK;
+    if (hipMalloc(&d_ws, nt::ws_bytes_per_slot() * ws_slots) != hipSuccess) {
+      (void)hipGetLastError();
+      d_ws = nullptr;
+      return NT_ENOMEM;
+    }
+    return NT_OK;
+  }
+
   // compute stream of chunk c
   hipStream_t cstr(int c) const { return (c & 1) ? stream2 : stream; }
 
@@ -262,7 +323,7 @@ struct Device {
     const int rc = grow_ws2(blocks);
     if (rc != NT_OK) return rc;
     if (hipStreamWaitEvent(stream2, ws2_done, 0) != hipSuccess ||
-        nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, ws2.p, (uint32_t)std::max<uint64_t>(blocks, 1),
+        nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, bbits, ws2.p, (uint32_t)std::max<uint64_t>(blocks, 1),
                           out, stream2) != hipSuccess ||
         hipEventRecord(ws2_done, stream2) != hipSuccess)
       return NT_EHIP;
@@ -320,7 +381,7 @@ struct Device {
     if (grow_ws2(ws_slots) != NT_OK) return hipErrorOutOfMemory;
     hipError_t e = hipStreamWaitEvent(s, ws2_done, 0);
     if (e != hipSuccess) return e;
-    e = nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, ws2.p, ws_slots, out, s);
+    e = nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, bbits, ws2.p, ws_slots, out, s);
     if (e != hipSuccess) return e;
     return hipEventRecord(ws2_done, s);
   }
@@ -331,7 +392,7 @@ struct Device {
                     hipStream_t s) {
     hipError_t e = hipStreamWaitEvent(s, ws_done, 0);
     if (e != hipSuccess) return e;
-    e = nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, d_ws, ws_slots, out, s);
+    e = nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, bbits, d_ws, ws_slots, out, s);
     if (e != hipSuccess) return e;
     return hipEventRecord(ws_done, s);
   }
@@ -357,6 +418,7 @@ struct NtSmallModel {
 
 struct nt_ctx {
   std::vector<std::unique_ptr<ntrt::Device>> devs;
+  uint64_t hbm_budget = 0;   // per device entry (Budget::limit); NT_HBM_BUDGET at init
   NtSmallModel small_model;  // written by nt_set_small_call_path before small_mode
   // small-call path (cpu_lane.hpp): NT_SMALL_OFF / AUTO / ALWAYS, host threads
   std::atomic<int> small_mode{NT_SMALL_OFF};
@@ -364,21 +426,26 @@ struct nt_ctx {
   std::atomic<uint64_t> calls_host{0}, calls_gpu{0};
 };
 
-struct nt_keyset {
-  nt_ctx* ctx = nullptr;
+namespace ntrt {
+// Device tables of a key set, shared by its nt_keyset handle and every
+// nt_committee built on it: a committee keeps them alive, so freeing the key set
+// before the committee is safe.  The key combs' bytes are reserved
+// in each device entry's budget while the tables live.
+struct KsTables {
   uint32_t nkeys = 0;
-  std::vector<uint8_t> enc;     // host copy of the key encodings (small-call path)
   int bits = 0;                 // comb digit width of every key (nt::kKeyComb{Wide,Mid,Narrow})
-  std::vector<uint32_t> flags;  // host copy of kKey* bits
   struct PerDev {
     int ordinal = -1;
     uint32_t* d_enc = nullptr;
     uint32_t* d_meta = nullptr;
     uint32_t* d_comb = nullptr;
+    std::shared_ptr<Budget> budget;
+    uint64_t reserved = 0;
   };
   std::vector<PerDev> dev;
-  ~nt_keyset() {
+  ~KsTables() {
     for (auto& d : dev) {
+      if (d.budget && d.reserved) d.budget->release(d.reserved);
       if (d.ordinal < 0) continue;
       (void)hipSetDevice(d.ordinal);
       if (d.d_enc) (void)hipFree(d.d_enc);
@@ -386,6 +453,16 @@ struct nt_keyset {
       if (d.d_comb) (void)hipFree(d.d_comb);
     }
   }
+};
+}  // namespace ntrt
+
+struct nt_keyset {
+  nt_ctx* ctx = nullptr;
+  uint32_t nkeys = 0;
+  std::vector<uint8_t> enc;     // host copy of the key encodings (small-call path)
+  int bits = 0;                 // = t->bits
+  std::vector<uint32_t> flags;  // host copy of kKey* bits
+  std::shared_ptr<ntrt::KsTables> t;
 };
 
 namespace ntrt {

@@ -34,7 +34,10 @@ EXPORTED = [
     "nt_keyset_free", "nt_keyset_flags", "nt_keyset_info", "nt_ed25519_verify_keyset", "nt_ed25519_verify_batch_groups_keyset",
     "nt_dev_ed25519_verify_keyset", "nt_host_alloc", "nt_host_free", "nt_set_small_call_path", "nt_call_counts",
     "nt_committee_create", "nt_committee_free", "nt_certificates_ingest", "nt_small_call_model",
+    "nt_set_hbm_budget", "nt_memory_info", "nt_dev_stream",
 ]
+MEMORY_INFO_KEYS = ("comb_b_bits", "comb_b_bytes", "key_comb_bytes", "workspace_bytes", "stash_bytes",
+                    "staging_bytes", "budget", "held")
 
 
 class NtError(RuntimeError):
@@ -89,6 +92,14 @@ def load_library(path=None):
     lib.nt_call_counts.argtypes = [_vp, _u64p, _u64p]
     if hasattr(lib, "nt_small_call_model"):  # absent from older A/B builds (NTCRYPTO_LIB)
         lib.nt_small_call_model.argtypes = [_vp, ctypes.POINTER(ctypes.c_double)]
+    lib.nt_committee_create.argtypes = [_vp, _vp, _u32p, _u64p, _u32p, ctypes.c_uint32, ctypes.POINTER(_vp)]
+    lib.nt_committee_free.argtypes = [_vp]
+    lib.nt_committee_free.restype = None
+    lib.nt_certificates_ingest.argtypes = [_vp, _vp, _u8p, _u64p, _u64p, _u64, _u64, _u8p]
+    if hasattr(lib, "nt_memory_info"):  # absent from round-3 A/B builds (NTCRYPTO_LIB)
+        lib.nt_set_hbm_budget.argtypes = [_vp, ctypes.c_uint64]
+        lib.nt_memory_info.argtypes = [_vp, ctypes.c_int, _u64p]
+        lib.nt_dev_stream.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_vp)]
     _lib = lib
     return lib
 
@@ -184,6 +195,24 @@ class Backend:
         d["threads"] = int(d["threads"])
         d["calibrated"] = bool(d["calibrated"])
         return d
+
+    def set_hbm_budget(self, nbytes):
+        """Cap the tables (comb of B + key combs) this context holds per device
+        entry; 0 = no cap (nt_set_hbm_budget)."""
+        _check(self.lib.nt_set_hbm_budget(self.ctx, int(nbytes)), "nt_set_hbm_budget")
+
+    def memory_info(self, dev=0):
+        """What device entry `dev` of this context holds (nt_memory_info)."""
+        out = np.zeros(8, np.uint64)
+        _check(self.lib.nt_memory_info(self.ctx, int(dev), _p(out, _u64p)), "nt_memory_info")
+        return dict(zip(MEMORY_INFO_KEYS, (int(x) for x in out)))
+
+    def dev_stream(self, dev=0, which=0):
+        """Raw hipStream_t of device entry `dev`'s compute stream `which` (0 / 1):
+        the two sit on hardware queues of their own (nt_dev_stream)."""
+        p = _vp()
+        _check(self.lib.nt_dev_stream(self.ctx, int(dev), int(which), ctypes.byref(p)), "nt_dev_stream")
+        return int(p.value)
 
     def call_counts(self):
         """(host-lane calls, GPU calls) of the host entry points so far."""
@@ -361,3 +390,47 @@ def default_backend():
     if _default is None:
         _default = Backend(0)
     return _default
+
+
+class Committee:
+    """A committee over a keyset (nt_committee_*): stake and worker ids per key,
+    the quorum threshold; ingest() runs Certificate::verify on wire bytes on the
+    device (nt_certificates_ingest).  It keeps the keyset's device tables alive:
+    the Keyset may be closed first."""
+
+    def __init__(self, keyset, stakes, workers, quorum):
+        self.be = keyset.be
+        stakes = np.ascontiguousarray(stakes, np.uint32)
+        wfirst = np.zeros(len(workers) + 1, np.uint64)
+        wfirst[1:] = np.cumsum([len(w) for w in workers])
+        wids = np.ascontiguousarray(np.concatenate([np.asarray(w, np.uint32) for w in workers] + [np.zeros(1, np.uint32)]),
+                                    np.uint32)
+        h = _vp()
+        _check(self.be.lib.nt_committee_create(self.be.ctx, keyset.h, _p(stakes, _u32p), _p(wfirst, _u64p),
+                                               _p(wids, _u32p), int(quorum), ctypes.byref(h)), "nt_committee_create")
+        self.h = h
+
+    def ingest(self, messages, gc_round=0):
+        """primary::DagError code per wire message (NT_DAG_HOST = 0xff: left to the host decoder)."""
+        n = len(messages)
+        ln = np.array([len(m) for m in messages], np.uint64)
+        off = np.zeros(n, np.uint64)
+        if n > 1:
+            off[1:] = np.cumsum(ln)[:-1]
+        data = np.frombuffer(b"".join(messages), np.uint8) if n else np.zeros(1, np.uint8)
+        data = data if len(data) else np.zeros(1, np.uint8)
+        out = np.zeros(max(n, 1), np.uint8)
+        _check(self.be.lib.nt_certificates_ingest(self.be.ctx, self.h, _p(data), _p(off, _u64p), _p(ln, _u64p), n,
+                                                  int(gc_round), _p(out)), "nt_certificates_ingest")
+        return out[:n]
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.be.lib.nt_committee_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

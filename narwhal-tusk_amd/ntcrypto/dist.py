@@ -49,3 +49,27 @@ def gather_bytes(local: bytes, world: int):
     out = [None] * world
     dist.all_gather_object(out, local)
     return out
+
+
+def gather_object(x, world: int = None):
+    """Every rank's picklable object on every rank (gloo all_gather_object;
+    called outside timed regions only)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [x]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, x)
+    return out
+
+
+def rank_summary(rows, rate_key="rate", time_key="kernel_ms"):
+    """Per-rank rows of one config plus the min / max / mean of its rate and
+    kernel time, so an N-rank line shows a slow rank or a straggling shard
+    instead of only the max-over-ranks wall time."""
+    rates = [r[rate_key] for r in rows]
+    times = [r[time_key] for r in rows]
+    return {"per_rank": rows,
+            rate_key + "_min": round(min(rates), 1), rate_key + "_max": round(max(rates), 1),
+            rate_key + "_mean": round(sum(rates) / len(rates), 1),
+            time_key + "_min": round(min(times), 3), time_key + "_max": round(max(times), 3),
+            "slowest_rank": rows[rates.index(min(rates))]["rank"]}

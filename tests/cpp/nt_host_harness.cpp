@@ -378,6 +378,10 @@ void nth_ks_plan(unsigned long long n, uint32_t cus, uint32_t cap, int force, ui
   const KsPlan p = ks_plan(n, cus, cap, force);
   out[0] = p.waves; out[1] = p.chunks; out[2] = p.base_rows; out[3] = p.extra; out[4] = p.per_simd; out[5] = p.rounds;
 }
+// the stash bound every plan of a launch of <= rows rows fits in (ks_plan.hpp)
+unsigned long long nth_ks_stash_rows_bound(unsigned long long rows, uint32_t cus) {
+  return ks_stash_rows_bound(rows, cus);
+}
 // streamed rows (ks_stream_plan): out = waves, rows, prow, per_simd
 void nth_ks_stream_plan(unsigned long long n, uint32_t cus, uint32_t cap, int force, uint32_t* out) {
   const KsPlan p = ks_stream_plan(n, cus, cap, force);

@@ -60,3 +60,18 @@ def test_two_rank_bench_on_one_gpu():
     assert d["n_gpus"] == 2 and d["parity"] == {"mismatches_vs_expected": 0, "checked": 2 * 8192}
     assert d["certificates"]["keyset"]["mismatches_vs_expected"] == 0
     assert d["sha512"]["spot_check_ok"]
+    # the whole metric near the front of the line, and every
+    # rank's share attributable (a slow rank would show in min / max)
+    keys = list(d)
+    assert keys.index("sha512_gbs") < 6 and keys.index("certs_per_s") < 6
+    assert d["sha512_gbs"] == d["sha512"]["value"] > 0 and d["certs_per_s"] == d["certificates"]["value"] > 0
+    pr = d["per_rank"]
+    for cfg, size in (("cfg2", "signatures"), ("cfg3", "certificates"), ("cfg4", "messages")):
+        rows = pr[cfg]["per_rank"]
+        assert sorted(r["rank"] for r in rows) == [0, 1], cfg
+        assert all(r["kernel_ms"] > 0 and r["rate"] > 0 for r in rows), cfg
+        assert pr[cfg]["rate_min"] <= pr[cfg]["rate_mean"] <= pr[cfg]["rate_max"], cfg
+        assert pr[cfg]["slowest_rank"] in (0, 1)
+    assert sum(r["certificates"] for r in pr["cfg3"]["per_rank"]) == 2000
+    assert sum(r["messages"] for r in pr["cfg4"]["per_rank"]) == 256
+    assert all(r["signatures"] == 8192 for r in pr["cfg2"]["per_rank"])

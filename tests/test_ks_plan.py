@@ -111,3 +111,33 @@ def test_stream_plan_config3_shards():
         p = stream_plan(certs * 68)
         assert p["waves"] == waves
         assert p["prow"] == math.ceil(p["rows"] / waves) + 2 <= 64
+
+
+def test_stash_bound_covers_every_smaller_launch():
+    """the host entry points size both stashes once for their
+    largest chunk and launch smaller chunks into them, so the stash size
+    (ks_stash_rows_bound, keyset_stash_bytes) must bound waves x stash rows of
+    EVERY plan of a launch of at most that many rows -- the chunked plan's own
+    figure is not monotone (36,864 rows on 256 CUs plan 18,432 stash rows with
+    2 waves per SIMD x 2 rounds; 30,720 rows plan 30,720 with 3 x 1)."""
+    lib = _hostarith.load()
+    lib.nth_ks_stash_rows_bound.restype = ctypes.c_ulonglong
+    bound = lambda rows, cus: lib.nth_ks_stash_rows_bound(ctypes.c_ulonglong(rows), cus)
+    def stash_rows(p):
+        return p["waves"] * (p["base"] + (1 if p["extra"] else 0))
+    # the worked example: the smaller launch needs the larger stash
+    assert stash_rows(plan(30_720 * 64, 256, 64, 0)) > stash_rows(plan(36_864 * 64, 256, 64, 0))
+    for cus in (4, 80, 256):
+        prev = 0
+        for rows in list(range(1, 3000, 37)) + [12_287, 12_288, 13_282, 26_563, 30_720, 36_864, 53_125, 106_250,
+                                                131_072]:
+            b = bound(rows, cus)
+            assert b >= prev  # monotone
+            prev = b
+            n = rows * 64
+            for cap in (1, 8, 26, 64):
+                for force in (0, 2, 3):
+                    p = plan(n, cus, cap, force)
+                    assert stash_rows(p) <= b, (rows, cus, cap, force)
+                    s = stream_plan(n, cus, cap, force)
+                    assert s["waves"] * s["prow"] <= b, (rows, cus, cap, force)

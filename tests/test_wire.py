@@ -372,3 +372,151 @@ def test_core_device_ingest_many_chunks(monkeypatch):
         assert len(counts) >= 5, counts
     finally:
         core.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_core_device_ingest_real_shape_vs_model(monkeypatch):
+    """VERDICT r03 item 5: Core::ingest_device at config 3's real shape -- an
+    n = 100 committee (quorum 67), 10,000 wire certificates with 32 payload
+    digests, 67 parents and 67-68 votes each (~11 KB per message) -- against
+    tests/_wire.py's model_sanitize driven by the CPU ORACLE's signature
+    verdicts (messages.rs:189-215, core.rs:338-346, primary.rs:225-244), not
+    against the host decoder.  Every error kind appears: forged votes, an
+    all-zero vote signature (crypto_tests.rs:96-115), repeated voters, voters
+    outside the committee or without stake, unknown and zero-stake authors,
+    bad header ids, worker ids the author does not have, bad header
+    signatures, too few votes, truncations, genesis certificates and rounds
+    below the GC round.  The signatures come from the GPU signer (pinned to
+    the oracle elsewhere); every verdict the model needs comes from the oracle."""
+    import hashlib
+    import ntcrypto
+    from _oracle import load
+    orc = load()
+    rng = random.Random(424242)
+    nk, G, gc_round = 100, 10_000, 50
+    be = ntcrypto.Backend(device=0)
+    try:
+        seeds = np.stack([np.frombuffer(hashlib.sha512(b"nt-ingest-key" + struct.pack("<Q", i)).digest()[:32],
+                                        np.uint8) for i in range(nk + 1)])
+        pks = be.sign_batch(seeds)
+        keys = [pks[i].tobytes() for i in range(nk)]
+        stranger = pks[nk].tobytes()                      # a key outside the committee
+        stakes = [1] * nk
+        stakes[nk - 1] = 0                                # an authority without voting rights
+        com = W.Committee(keys, stakes, [1] * nk)         # one worker (id 0) per authority
+        quorum = com.quorum()
+        assert quorum == 67                               # 2 * 99 // 3 + 1 (stake 99 in total)
+        kidx = {k: i for i, k in enumerate(keys)}
+        kidx[stranger] = nk
+        kinds = [g % 24 for g in range(G)]               # 0 and 15..23: valid certificates
+        rng.shuffle(kinds)
+        certs, tasks = [], []   # tasks: (key index, message) to sign on the GPU
+        for g in range(G):
+            k = kinds[g]
+            author = keys[rng.randrange(nk - 1)]
+            if k == 11:
+                author = stranger
+            elif k == 12:
+                author = keys[nk - 1]
+            rnd = gc_round + rng.randrange(0, 5) if k != 8 else gc_round - 1 - rng.randrange(3)
+            payload = {_rb(rng, 32): 0 for _ in range(32)}
+            if k == 5:
+                payload[_rb(rng, 32)] = 1                 # a worker id the author does not have
+            h = W.Header(author, rnd, payload, {_rb(rng, 32) for _ in range(67)})
+            if k == 4:
+                h.id = _rb(rng, 32)
+            if k == 7:                                    # genesis: round 0, zero id, no votes
+                h = W.Header(keys[rng.randrange(nk)], 0, {}, set(), id_=bytes(32))
+                certs.append(W.Certificate(h, []))
+                continue
+            tasks.append((kidx[author], h.id))
+            voters = rng.sample(keys[:nk - 1], quorum + rng.randrange(0, 2))
+            if k == 9:
+                voters = voters[:quorum - 1]
+            elif k == 2:
+                voters[5] = voters[1]                     # a repeated voter
+            elif k == 3:
+                voters[7] = stranger
+            elif k == 13:
+                voters[3] = keys[nk - 1]
+            c = W.Certificate(h, [(v, None) for v in voters])
+            d = c.digest()
+            for v in voters:
+                tasks.append((kidx[v], d))
+            certs.append(c)
+        # GPU-sign every header id and vote digest, then fill the signatures in
+        msg = np.frombuffer(b"".join(m for _, m in tasks), np.uint8)
+        _, sig = be.sign_batch(seeds[[i for i, _ in tasks]], msg, np.arange(len(tasks), dtype=np.uint64) * 32,
+                               np.full(len(tasks), 32, np.uint64))
+        t = 0
+        for g, c in enumerate(certs):
+            if not c.votes and c.header.round == 0:
+                continue
+            c.header.sig = sig[t].tobytes()
+            t += 1
+            c.votes = [(v, sig[t + j].tobytes()) for j, (v, _) in enumerate(c.votes)]
+            t += len(c.votes)
+            k = kinds[g]
+            if k == 1:                                    # a forged vote
+                j = rng.randrange(len(c.votes))
+                s = bytearray(c.votes[j][1])
+                s[rng.randrange(64)] ^= 1 << rng.randrange(8)
+                c.votes[j] = (c.votes[j][0], bytes(s))
+            elif k == 10:                                 # a forged header signature
+                s = bytearray(c.header.sig)
+                s[rng.randrange(64)] ^= 1 << rng.randrange(8)
+                c.header.sig = bytes(s)
+            elif k == 14:                                 # Signature::default() as a vote
+                c.votes[9] = (c.votes[9][0], bytes(64))
+        wires = []
+        for g, c in enumerate(certs):
+            m = W.message(c)
+            if kinds[g] == 6:
+                m = m[:rng.randrange(1, len(m))]          # truncated on the wire
+            wires.append(m)
+        # the oracle's verdict for every signature the model can ask about
+        hs = [c for g, c in enumerate(certs) if kinds[g] != 6 and c.votes]
+        hpk = np.stack([np.frombuffer(c.header.author, np.uint8) for c in hs])
+        hsig = np.stack([np.frombuffer(c.header.sig, np.uint8) for c in hs])
+        hmsg = np.frombuffer(b"".join(c.header.id for c in hs), np.uint8)
+        sv = orc.verify_strict_many(hpk, hsig, hmsg, np.arange(len(hs), dtype=np.uint64) * 32,
+                                    np.full(len(hs), 32, np.uint64), nthreads=16)
+        strict_v = {(c.header.id, c.header.author, c.header.sig): bool(v) for c, v in zip(hs, sv)}
+        cnt = np.array([len(c.votes) for c in hs], np.uint32)
+        first = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.uint64)
+        vpk = np.stack([np.frombuffer(pk, np.uint8) for c in hs for pk, _ in c.votes])
+        vsig = np.stack([np.frombuffer(s, np.uint8) for c in hs for _, s in c.votes])
+        dig = np.stack([np.frombuffer(c.digest(), np.uint8) for c in hs])
+        bv, _ = orc.verify_batch_groups(vpk, vsig, first, cnt, dig, nthreads=16)
+        batch_v = {c.digest(): bool(v) for c, v in zip(hs, bv)}
+        names = N.DAG_ERRORS
+        # twice: at GC round 50 (rounds 47-49 are TooOld, so is every genesis
+        # certificate: sanitize_certificate's round filter runs before
+        # Certificate::verify) and at GC round 0 (genesis accepted, core.rs:339-346)
+        seen = set()
+        for gc in (gc_round, 0):
+            expect = [W.model_sanitize(com, gc, None, c, lambda d, pk, s: strict_v[(d, pk, s)],
+                                       lambda d, votes: batch_v[d]) if kinds[g] != 6 else W.SERIALIZATION_ERROR
+                      for g, c in enumerate(certs)]
+            seen |= {names[e] for e in expect}
+            core = N.Core(np.frombuffer(b"".join(keys), np.uint8), stakes, [1] * nk, gc, None, True)
+            try:
+                got, host = core.ingest(*N.pack(wires), threads=8, device=True)
+            finally:
+                core.close()
+            diff = [(g, kinds[g], names[x], names[y]) for g, (x, y) in enumerate(zip(got, expect)) if x != y]
+            assert not diff, (gc, diff[:10])
+            # the device decides every certificate in canonical form with committee keys;
+            # truncated messages (kind 6) and the ones naming a stranger (3, 11) go to the host
+            routed = sum(1 for k in kinds if k in (3, 6, 11))
+            print("gc_round %d: host_decided %d of %d (truncated / stranger keys: %d); verdicts %s"
+                  % (gc, host, G, routed, {names[x]: int((np.array(expect) == x).sum()) for x in set(expect)}))
+            assert host <= routed
+            assert sum(e == W.OK for e in expect) > G // 4
+            if gc == 0:
+                assert all(expect[g] == W.OK for g in range(G) if kinds[g] == 7)  # genesis
+        assert seen == {"Ok", "InvalidSignature", "InvalidHeaderId", "MalformedHeader", "UnknownAuthority",
+                        "AuthorityReuse", "CertificateRequiresQuorum", "TooOld", "SerializationError"}, seen
+    finally:
+        be.close()
