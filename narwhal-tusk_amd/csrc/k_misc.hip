@@ -537,9 +537,11 @@ static bool keyset_stream_enabled() {
 }
 
 KsPlan keyset_plan(uint64_t n, uint32_t cus) {
-  static const int force = env_occ("NT_KEYSET_WAVES", 0, 2, 3);
+  // 1 (streamed plan only): one wave per SIMD per launch, for launches that
+  // overlap another stream's on the same SIMDs (A/B)
+  static const int force = env_occ("NT_KEYSET_WAVES", 0, 1, 3);
   return keyset_stream_enabled() ? ks_stream_plan(n, cus, keyset_per_lane(), force)
-                                 : ks_plan(n, cus, keyset_per_lane(), force);
+                                 : ks_plan(n, cus, keyset_per_lane(), force == 1 ? 2 : force);
 }
 
 hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,

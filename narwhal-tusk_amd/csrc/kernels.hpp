@@ -36,7 +36,7 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
 // scratch of launch_verify_keyset: the chunk counter and the key-grouped order (d_sort, required)
 size_t keyset_sort_bytes(uint64_t n);
 // the plan of one key-cache launch over n signatures on a device of `cus` CUs (ks_plan.hpp;
-// NT_KEYSET_WAVES = 2 / 3 forces the waves per SIMD, NT_KEYSET_PER_LANE caps the rows per chunk)
+// NT_KEYSET_WAVES = 1 (streamed) / 2 / 3 forces the waves per SIMD, NT_KEYSET_PER_LANE caps the rows per chunk)
 KsPlan keyset_plan(uint64_t n, uint32_t cus);
 // signatures one full round of the launch covers (host-side chunk sizing)
 uint64_t keyset_round_sigs(uint32_t cus);
