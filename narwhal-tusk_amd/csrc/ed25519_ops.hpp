@@ -359,14 +359,25 @@ NT_HD NT_INLINE void ladder_ar(ge_cp& t, const uint32_t ud[8], const uint32_t vd
   }
 }
 
-// k = SHA-512(R || A || M) mod L over the raw encodings (Scalar::from_hash)
+// k = SHA-512(R || A || M) mod L over the raw encodings (Scalar::from_hash).
+// kDigestFast: a 32-byte M (what every certificate, header and vote signs)
+// hashes as one block built from registers (sha512_96) -- the key-cache
+// kernels; the general verify kernel keeps one code path (config 2 signs 512-B
+// messages, and its register budget is tight).
+template <bool kDigestFast = false>
 NT_HD NT_INLINE void hram_scalar(uint32_t k[8], const uint32_t Rw[8], const uint32_t Aw[8], const uint8_t* msg,
                                  uint64_t len) {
   uint32_t prefix[16];
 #pragma unroll
   for (int q = 0; q < 8; ++q) { prefix[q] = Rw[q]; prefix[8 + q] = Aw[q]; }
   uint64_t st[8];
-  sha512_prefixed<16>(st, prefix, msg, len);
+  if (kDigestFast && len == 32) {
+    uint32_t m[8];
+    load_words<8>(m, msg);
+    sha512_96(st, prefix, m);
+  } else {
+    sha512_prefixed<16>(st, prefix, msg, len);
+  }
   uint32_t hw[16];
   sha512_out_words(hw, st, 16);
   sc_reduce512(k, hw);
@@ -490,7 +501,7 @@ NT_HD NT_INLINE uint32_t cached_point(ge_p3& acc, uint32_t meta, const uint32_t 
   uint32_t okj = sc_is_canonical(Sw) & (meta & kKeyDecodes ? 1u : 0u);
   if (is_strict<MODE>(meta)) okj &= (meta & kKeySmallOrder) ? 0u : 1u;
   uint32_t k[8];
-  hram_scalar(k, Rw, Aw, msg, len);
+  hram_scalar<true>(k, Rw, Aw, msg, len);
   wcomb_acc<WCombA, true>(acc, k, ca);
   wcomb_acc(acc, Sw, cb);
   return okj;

@@ -362,6 +362,24 @@ NT_HD NT_INLINE void sha512_prefixed(uint64_t st[8], const uint32_t* prefix, con
   }
 }
 
+// k = H(R || A || M) for a 32-byte M (every key-cache signature: headers, votes and
+// certificates sign a 32-byte digest, crypto/src/lib.rs:185-204): the 96 bytes
+// are one block built straight from registers -- no byte-granular tail assembly
+// (679 VALU in the key-cache kernel's ISA for the general path).
+NT_HD NT_INLINE void sha512_96(uint64_t st[8], const uint32_t prefix[16], const uint32_t m[8]) {
+  sha512_init(st);
+  uint32_t blk[32];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) blk[i] = prefix[i];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) blk[16 + i] = m[i];
+  blk[24] = 0x80u;  // the padding bit right after byte 95
+#pragma unroll
+  for (int i = 25; i < 31; ++i) blk[i] = 0u;
+  blk[31] = bswap32(96u * 8u);  // 128-bit big-endian bit length 768
+  sha512_compress_words(st, blk);
+}
+
 // First 32 bytes / all 64 bytes of the digest as little-endian memory words.
 NT_HD NT_INLINE void sha512_out_words(uint32_t* out, const uint64_t st[8], int nwords) {
   for (int i = 0; i < nwords / 2; ++i) {

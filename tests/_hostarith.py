@@ -170,6 +170,12 @@ def sha512(m):
     return o.raw
 
 
+def hram(sig, pk, msg, fast):
+    o = ctypes.create_string_buffer(32)
+    load().nth_hram(sig, pk, msg, ctypes.c_uint64(len(msg)), int(fast), o)
+    return o.raw
+
+
 def counts_reset():
     load().nth_counts_reset()
 

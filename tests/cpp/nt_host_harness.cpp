@@ -207,6 +207,15 @@ void nth_sha512(const uint8_t* msg, uint64_t len, uint8_t* out64) {
   sha512_out_words(w, st, 16);
   std::memcpy(out64, w, 64);
 }
+// k = H(R || A || M) mod L through the general and the one-block (32-byte M) paths
+void nth_hram(const uint8_t* sig, const uint8_t* pk, const uint8_t* msg, uint64_t len, int fast, uint8_t* out32) {
+  alignas(16) uint32_t A[8], S[16], k[8];
+  std::memcpy(A, pk, 32);
+  std::memcpy(S, sig, 64);
+  if (fast) hram_scalar<true>(k, S, A, msg, len);
+  else hram_scalar<false>(k, S, A, msg, len);
+  std::memcpy(out32, k, 32);
+}
 int nth_verify(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint64_t len) {
   alignas(16) uint32_t A[8], S[16];
   std::memcpy(A, pk, 32);

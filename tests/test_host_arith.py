@@ -95,6 +95,20 @@ def test_sha512_host_build():
         assert H.sha512(m) == hashlib.sha512(m).digest()
 
 
+def test_hram_one_block_path_matches_hashlib():
+    """hram_scalar<true> (the key-cache kernels: a 32-byte message hashed as one
+    block built from registers) and the general path both equal
+    SHA-512(R || A || M) mod L; other lengths fall through to the general path."""
+    rng = random.Random(96)
+    for n in (32, 32, 32, 0, 31, 33, 64):
+        sig = bytes(rng.getrandbits(8) for _ in range(64))
+        pk = bytes(rng.getrandbits(8) for _ in range(32))
+        m = bytes(rng.getrandbits(8) for _ in range(n))
+        want = (int.from_bytes(hashlib.sha512(sig[:32] + pk + m).digest(), "little") % H.L).to_bytes(32, "little")
+        assert H.hram(sig, pk, m, True) == want, n
+        assert H.hram(sig, pk, m, False) == want, n
+
+
 def test_corpus_through_device_code():
     d = np.load(os.path.join(GOLD, "ed25519_corpus.npz"))
     for i in range(len(d["cat"])):
