@@ -166,6 +166,16 @@ def fork_join(streams, stream):
     return fork, join
 
 
+_T0 = time.time()
+
+
+def progress(what):
+    """one stderr line per finished phase (rank 0): a long default run keeps
+    writing, and the log shows where the time went"""
+    if os.environ.get("RANK", "0") == "0":
+        print("[bench %6.1fs] %s" % (time.time() - _T0, what), file=sys.stderr, flush=True)
+
+
 def free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -189,6 +199,10 @@ def rank_launch(argv, n, port, env=None):
 
 def main():
     args = parse()
+    if os.environ.get("NT_BENCH_STACKS"):
+        # diagnostics: every thread's Python stack to stderr every N seconds
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["NT_BENCH_STACKS"]), repeat=True)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # nothing here has initialised the GPU: start the ranks as a child and
         # report its status (no exec from this process)
@@ -250,6 +264,7 @@ def main():
                 sig.data_ptr())
     torch.cuda.synchronize(dev)
     gen_s = time.time() - t0
+    progress("cfg2 inputs signed on the GPU (%.1f s)" % gen_s)
 
     # 1 % edge cases from the golden corpus (512-B entries), evenly over categories
     corpus = np.load(os.path.join(ROOT, "tests", "golden", "ed25519_corpus.npz"))
@@ -327,6 +342,7 @@ def main():
         got = np.unpackbits(o.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
         mism += int((got != expect).sum())
     mism = int(max_over_ranks(mism))
+    progress("cfg2 timed: %.1f M verifies/s" % (n * world * args.steps / max_over_ranks(wall) / 1e6))
 
     total = n * world * args.steps
     value = total / wall
@@ -388,6 +404,7 @@ def main():
     if nstreams == 1 and os.environ.get("NT_BENCH_CFG2_PIPE", "1") != "0":
         line["two_streams"] = cfg2_two_streams(torch, be, dev, stream, ntcrypto, pk, sig, msgs, off, ln, n, words,
                                                expect, args, barrier, max_over_ranks, world)
+        progress("cfg2 two streams")
 
     # ------------------------------------------- same cfg2 batch through the host entry point
     # (caller buffers in ordinary host memory: PCIe-inclusive, never `value`)
@@ -422,33 +439,40 @@ def main():
                                   "note": "inputs in nt_host_alloc memory (what a caller that owns its receive "
                                           "buffers can do): DMA straight from them"}
     del pk_p, sig_p, msg_p
+    progress("cfg2 host entry point")
 
     # ------------------------------------------------- small calls: per-call latency
     if not args.no_latency:
         line["latency"] = bench_latency(be, pk_h, sig_h, msg_h, L)
+        progress("lone-call latency")
 
     # ----------------------- worker digest batching (§8(f).3) and device-slot contention
     if not args.no_latency and world == 1:
         line["digest_batcher"] = bench_batcher()
         line["contention"] = bench_contention(ntcrypto, local)
+        progress("digest batcher, contention")
 
     # ---------------------------------------------------------------- config 4: SHA-512 GB/s
     if not args.no_sha:
         line["sha512"] = bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_ranks)
         line["sha512"]["real_batch"] = bench_sha_real(args, torch, dev, be, sp, stream, world, rank, barrier,
                                                       max_over_ranks)
+        progress("cfg4 SHA-512: %.0f GB/s" % line["sha512"]["value"])
 
     # ---------------------------------------------------------------- config 3: certificates
     if not args.no_certs:
         line["certificates"] = bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_ranks)
+        progress("cfg3 certificates: %.2f M/s" % (line["certificates"]["value"] / 1e6))
 
     # ---------------------------------------------------------------- §8(f).2: wire ingestion
     if not args.no_ingest:
         line["ingest"] = bench_ingest(args, be, world, rank, local, max_over_ranks, barrier)
+        progress("cfg3 wire ingestion")
 
     # ---------------------------------------------------------------- CPU baseline (rank 0, N=1)
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args, pk_h, sig_h, msg_h, L, got)
+        progress("CPU baselines")
 
     if "sha512" in line:
         line["sha512_gbs"] = line["sha512"]["value"]
@@ -487,6 +511,7 @@ def cfg2_two_streams(torch, be, dev, stream, ntcrypto, pk, sig, msgs, off, ln, n
         be.dev_verify(0, streams[i % 2].cuda_stream, ntcrypto.NT_MODE_STRICT, pk.data_ptr(), sig.data_ptr(),
                       msgs.data_ptr(), off.data_ptr(), ln.data_ptr(), n, outs[i % 2].data_ptr())
 
+    barrier()  # outs (zeroed on `stream`) are written on the pipeline streams
     for i in range(max(2, args.warmup)):
         step(i)
     barrier()
@@ -752,6 +777,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
     t_ks = time.perf_counter()
     ks = be.keyset(pks)
     ks_build_s = time.perf_counter() - t_ks
+    progress("cfg3 committee key cache built (%.1f s)" % ks_build_s)
     ks_bits, ks_bytes = ks.info()
     pks_d = torch.from_numpy(pks).to(dev)
     g = torch.Generator(device=dev)
@@ -901,12 +927,17 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
         return gb & hb & idok
 
     out = {}
-    steps = max(1, min(args.steps, 5))
     runs = [("keyset", True, nst)] + ([("keyset_one_stream", True, 1)] if nst > 1 and fused else []) + \
         [("uncached", False, 1)]
     for key, cached, ns in runs:
+        # up to 10 pipelined key-cache steps (a 2-stream pipeline's fill and drain are
+        # one step each); the uncached reference (~70 ms per step) keeps 5
+        steps = max(1, min(args.steps, 10 if cached else 5))
         mode_streams[cached] = ns
         kev.clear()
+        # the inputs and buffers were written on `stream`: the pipeline streams
+        # (library streams on queues of their own) must not start before that work
+        barrier()
         for i in range(max(1, args.warmup)):
             step(cached, i)
         barrier()
@@ -944,6 +975,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
             ach = rf["mads_per_signature"] * (V + G) / (own * 1e-3) / 1e12
             rf["launch_ms_one_stream"] = round(own, 3)
             rf["frac_one_stream_launch"] = round(ach / MAD_PEAK_TS, 4)
+        progress("cfg3 %s: %.2f M certificates/s" % (key, out[key]["certs_per_s"] / 1e6))
     if world == 1 and fused and os.environ.get("NT_BENCH_SHARDS", "1") != "0":
         out["shard_of"] = bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, stream, barrier, G, quorum,
                                             dict(hdr_flat=hdr_flat, h_off=h_off, h_len=h_len, cpre=cpre, c_off=c_off,
@@ -951,6 +983,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                                                  v_off=v_off, v_len=v_len, i_off=i_off, i_len=i_len, first=first,
                                                  cnt=cnt),
                                             expect, out["keyset"]["certs_per_s"])
+        progress("cfg3 shards")
     ks.close()
     if world == 1 and not getattr(args, "no_cpu", False):
         out["cpu_baseline"] = cert_cpu_baseline(args, hdr, hlen, ids, tmp_pk, hsig, cpre, vpk, vsig, quorum, expect)
@@ -987,7 +1020,7 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, stream, barri
     aggregate this GPU's shard rate implies (the 8-GPU run itself is the
     driver's)."""
     res = {}
-    steps = max(1, min(args.steps, 5))
+    steps = max(1, min(args.steps, 10))
     nst = len(streams)
     for N in (2, 4, 8):
         Gs = G // N
@@ -1005,6 +1038,10 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, stream, barri
             b["msgbuf"][Gs:] = t["ids"][:Gs]
             bufs.append(b)
         kev = []
+        # mkey / msig / m_off / m_len and the buffers above were built on `stream`;
+        # the pipeline streams read them (an unfinished m_off is a wild message
+        # offset: the key-cache kernel reads out of bounds)
+        barrier()
 
         def step(i, timed=False):
             st = streams[i % nst]
@@ -1472,6 +1509,7 @@ def cpu_baseline(args, pk_h, sig_h, msg_h, L, got):
            "host": host, "full_host_estimate": full_host(sample / dt, th, host),
            "single_thread_us_per_verify": round(per * 1e6, 2),
            "verdicts_agree_with_gpu": "%d/%d" % (agree, sample)}
+    progress("cfg2 CPU baseline")
     ext = sodium_baseline(orc, pk_h, sig_h, msg_h, L, got, th, args.cpu_seconds)
     if ext:
         out["external"] = ext

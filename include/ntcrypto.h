@@ -263,7 +263,11 @@ void nt_host_free(void *p);
  * kernels then run strictly in order.  nt_dev_stream returns device entry
  * `dev`'s two compute streams (which = 0 / 1), created on queues of their own
  * (a CU-masked stream never shares its queue; the mask enables every CU): a
- * caller pipelining device-API batches should alternate between them. */
+ * caller pipelining device-API batches should alternate between them.  They
+ * are ordered against no other stream: inputs produced elsewhere (a framework's
+ * stream, a copy) must be complete -- an event the stream waits on, or a
+ * synchronize -- before the first call that reads them.  The kernels trust
+ * d_off / d_len; an offset read before it was written is a wild access. */
 int nt_dev_stream(nt_ctx *ctx, int dev, int which, void **out);
 int nt_dev_sha512_trunc32(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_data,
                           const uint64_t *d_off, const uint64_t *d_len, uint64_t n,

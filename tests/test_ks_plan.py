@@ -139,5 +139,6 @@ def test_stash_bound_covers_every_smaller_launch():
                 for force in (0, 2, 3):
                     p = plan(n, cus, cap, force)
                     assert stash_rows(p) <= b, (rows, cus, cap, force)
+                for force in (0, 1, 2, 3):  # 1: NT_KEYSET_WAVES=1, streamed plan only
                     s = stream_plan(n, cus, cap, force)
                     assert s["waves"] * s["prow"] <= b, (rows, cus, cap, force)
