@@ -132,10 +132,24 @@ struct Budget {
 // (rocprofv3 kernel trace, profiles/r04/): the bench's two config-3 streams
 // both landed on one queue and consecutive key-cache launches never
 // overlapped.  A stream created with a CU mask is never given a shared queue;
-// the mask here enables every CU.  NT_SHARED_QUEUES=1 restores plain streams.
-inline hipError_t compute_stream(hipStream_t* s, uint32_t cus) {
-  const char* e = std::getenv("NT_SHARED_QUEUES");
-  if (e && *e == '1') return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+// the mask here enables every CU.  NT_STREAMS selects the kind (A/B):
+// mask (default), plain (may share a queue; NT_SHARED_QUEUES=1 too), prio
+// (plain, the second stream at the highest priority: HIP keeps a queue pool
+// per priority, so the two never share one).
+inline hipError_t compute_stream(hipStream_t* s, uint32_t cus, int which) {
+  static const int kind = [] {
+    const char* q = std::getenv("NT_SHARED_QUEUES");
+    if (q && *q == '1') return 1;
+    const char* e = std::getenv("NT_STREAMS");
+    if (!e) return 0;
+    return std::strcmp(e, "plain") == 0 ? 1 : std::strcmp(e, "prio") == 0 ? 2 : 0;
+  }();
+  if (kind == 1 || (kind == 2 && which == 0)) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  if (kind == 2) {
+    int lo = 0, hi = 0;
+    const hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    return e != hipSuccess ? e : hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+  }
   std::vector<uint32_t> mask((cus + 31) / 32, 0xffffffffu);
   if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
   return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
@@ -232,9 +246,9 @@ struct Device {
       cstream = stream2 = stream;
     } else {
       // the two compute streams on hardware queues of their own (compute_stream)
-      NT_TRY(compute_stream(&stream, (uint32_t)prop.multiProcessorCount));
+      NT_TRY(compute_stream(&stream, (uint32_t)prop.multiProcessorCount, 0));
       NT_TRY(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
-      NT_TRY(compute_stream(&stream2, (uint32_t)prop.multiProcessorCount));
+      NT_TRY(compute_stream(&stream2, (uint32_t)prop.multiProcessorCount, 1));
     }
     NT_TRY(hipEventCreateWithFlags(&ws_done, hipEventDisableTiming));
     NT_TRY(hipEventCreateWithFlags(&stash_done, hipEventDisableTiming));

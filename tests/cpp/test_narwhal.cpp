@@ -362,6 +362,7 @@ TEST(committee_keyset_index_and_verify) {
 }
 
 int main(int argc, char** argv) {
+  std::setvbuf(stdout, nullptr, _IOLBF, 0);  // one line per test, also into a file
   for (int i = 1; i < argc; ++i) g_golden_pk.push_back(argv[i]);
   if (g_golden_pk.size() != 4) {
     std::printf("usage: test_narwhal pk0 pk1 pk2 pk3\n");
