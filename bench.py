@@ -135,17 +135,16 @@ def full_host(rate, threads, host):
 
 
 def pipeline_streams(torch, be, dev, stream, n):
-    """The n streams consecutive steps alternate between.  n = 2: the library's
-    two compute streams (nt_dev_stream), created on hardware queues of their
-    own -- two torch pool streams can share one queue (HIP multiplexes a
-    process's streams over GPU_MAX_HW_QUEUES = 4), and then their kernels run
-    strictly in order: the round-3 bench's config-3 streams did (rocprofv3
-    kernel trace, profiles/r04/).  NT_BENCH_TORCH_STREAMS=1 (A/B): torch's own."""
+    """The n streams consecutive steps alternate between: `stream` and n - 1
+    more torch streams (each on a hardware queue HIP picks).
+    NT_BENCH_LIB_STREAMS=1 (A/B): the library's two compute streams
+    (nt_dev_stream) -- measured 3-5 % slower for the same launches, one stream
+    or two (profiles/r04/ab_streams.txt)."""
     if n == 1:
         return [stream]
-    if os.environ.get("NT_BENCH_TORCH_STREAMS") == "1" or not hasattr(be, "dev_stream"):
-        return [stream] + [torch.cuda.Stream(dev) for _ in range(n - 1)]
-    return [torch.cuda.ExternalStream(be.dev_stream(0, k), device=dev) for k in range(n)]
+    if os.environ.get("NT_BENCH_LIB_STREAMS") == "1" and hasattr(be, "dev_stream"):
+        return [torch.cuda.ExternalStream(be.dev_stream(0, k), device=dev) for k in range(n)]
+    return [stream] + [torch.cuda.Stream(dev) for _ in range(n - 1)]
 
 
 def fork_join(streams, stream):
@@ -497,9 +496,8 @@ def main():
 
 def cfg2_two_streams(torch, be, dev, stream, ntcrypto, pk, sig, msgs, off, ln, n, words, expect, args, barrier,
                      max_over_ranks, world):
-    """Config 2 with consecutive 1M batches alternating between the library's
-    two compute streams (hardware queues of their own, nt_dev_stream): the
-    next batch's waves take the SIMDs the previous batch's last round leaves
+    """Config 2 with consecutive 1M batches alternating between two streams
+    (pipeline_streams): the next batch's waves take the SIMDs the previous batch's last round leaves
     idle (1M signatures are 15.26 signature slots per SIMD lane, run as 16:
     DESIGN.md §10).  Reported beside the one-stream headline, verdicts of both
     output buffers checked."""
@@ -533,8 +531,8 @@ def cfg2_two_streams(torch, be, dev, stream, ntcrypto, pk, sig, msgs, off, ln, n
     return {"verifies_per_s": round(n * world * args.steps / wall, 1), "ms_per_step": round(wall * 1e3 / args.steps, 3),
             "gpu_ms_per_step": round(ev0.elapsed_time(ev1) / args.steps, 3),
             "mismatches_vs_expected": int(max_over_ranks(mism)),
-            "note": "consecutive 1M batches alternating between the library's two compute streams "
-                    "(nt_dev_stream: each on a hardware queue of its own); the headline `value` is one stream, "
+            "note": "consecutive 1M batches alternating between two streams on different hardware queues; "
+                    "the headline `value` is one stream, "
                     "launches strictly back to back"}
 
 

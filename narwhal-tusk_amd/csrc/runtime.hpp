@@ -125,17 +125,18 @@ struct Budget {
   }
 };
 
-// A compute stream with a hardware queue of its own.  HIP multiplexes a
-// process's streams over GPU_MAX_HW_QUEUES (4) queues of each priority and,
-// once they exist, hands a new stream the least-used one, so two streams can
-// share a queue -- and kernels of one queue run back to back: measured
-// (rocprofv3 kernel trace, profiles/r04/): the bench's two config-3 streams
-// both landed on one queue and consecutive key-cache launches never
-// overlapped.  A stream created with a CU mask is never given a shared queue;
-// the mask here enables every CU.  NT_STREAMS selects the kind (A/B):
-// mask (default), plain (may share a queue; NT_SHARED_QUEUES=1 too), prio
-// (plain, the second stream at the highest priority: HIP keeps a queue pool
-// per priority, so the two never share one).
+// The device entry's two compute streams.  HIP multiplexes a process's
+// streams over GPU_MAX_HW_QUEUES (4) queues per priority and hands a new stream
+// the least-used one, so two streams can share a queue, and then their kernels
+// run strictly in order.  NT_STREAMS selects the kind: mask (default: a CU
+// mask enabling every CU -- a masked stream gets a queue of its own, so the
+// library's streams leave the shared queues to the caller's), plain (may share
+// a queue; NT_SHARED_QUEUES=1 too), prio (the second stream at the highest
+// priority: HIP keeps a queue pool per priority).  Measured (one box, two
+// rounds each; profiles/r04/ab_streams.txt): with the mask, a caller
+// pipelining on its own (torch) streams gets config 3 at 12.6 M/s and config
+// 2's two-stream line at 101.9 M/s; with plain library streams 12.6 and 96.5
+// (the caller's two streams no longer overlap).
 inline hipError_t compute_stream(hipStream_t* s, uint32_t cus, int which) {
   static const int kind = [] {
     const char* q = std::getenv("NT_SHARED_QUEUES");
@@ -245,7 +246,7 @@ struct Device {
       NT_TRY(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
       cstream = stream2 = stream;
     } else {
-      // the two compute streams on hardware queues of their own (compute_stream)
+      // the two compute streams (compute_stream)
       NT_TRY(compute_stream(&stream, (uint32_t)prop.multiProcessorCount, 0));
       NT_TRY(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
       NT_TRY(compute_stream(&stream2, (uint32_t)prop.multiProcessorCount, 1));
