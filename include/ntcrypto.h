@@ -263,7 +263,10 @@ void nt_host_free(void *p);
  * kernels then run strictly in order.  nt_dev_stream returns device entry
  * `dev`'s two compute streams (which = 0 / 1), created on queues of their own
  * (a CU-masked stream never shares its queue; the mask enables every CU): a
- * caller pipelining device-API batches should alternate between them.  They
+ * caller pipelining device-API batches may alternate between them or between
+ * two streams of its own (with the library's streams on queues of their own,
+ * the caller's two get separate shared queues; measured, the same launches ran
+ * 3-5 % faster on the caller's torch streams: DESIGN.md §8).  They
  * are ordered against no other stream: inputs produced elsewhere (a framework's
  * stream, a copy) must be complete -- an event the stream waits on, or a
  * synchronize -- before the first call that reads them.  The kernels trust
