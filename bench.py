@@ -165,6 +165,20 @@ def fork_join(streams, stream):
     return fork, join
 
 
+def side_streams(torch, dev, n):
+    """Streams for the header-id digests of the pipelined config-3 steps (one per
+    pipeline slot, the highest priority: HIP keeps a queue pool per priority,
+    so they never share a queue with a pipeline stream).  The header ids are
+    only needed by the verdict, so their 3.3 KB serial SHA-512 chains run beside
+    the signature launches instead of between two of them on the pipeline
+    stream; NT_BENCH_SIDE=0: on the pipeline stream, after the
+    signature launch (A/B)."""
+    if n < 2 or os.environ.get("NT_BENCH_SIDE", "1") == "0":
+        return None
+    lo, hi = torch.cuda.Stream.priority_range()
+    return [torch.cuda.Stream(dev, priority=hi) for _ in range(n)]
+
+
 _T0 = time.time()
 
 
@@ -835,6 +849,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
     # on one stream.
     nst = 2 if os.environ.get("NT_BENCH_STREAMS", "2") != "1" else 1
     streams = pipeline_streams(torch, be, dev, stream, nst)
+    side = side_streams(torch, dev, nst)
 
     def make_bufs():
         b = {"hd2": torch.empty((G, 32), dtype=torch.uint8, device=dev),
@@ -896,11 +911,20 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
             if timed:
                 kev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
                 kev[-1][0].record(st)
+            if side and slots(cached) > 1:
+                # header ids beside the signature launch; the step's last kernel waits for them
+                be.dev_sha512(0, side[k].cuda_stream, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G,
+                              b["hd2"].data_ptr())
+                hev = torch.cuda.Event()
+                hev.record(side[k])
             ks.dev_verify(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(),
                           m_off.data_ptr(), m_len.data_ptr(), V + G, b["mbits"].data_ptr())
             if timed:
                 kev[-1][1].record(st)
-            be.dev_sha512(0, sq, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, b["hd2"].data_ptr())
+            if side and slots(cached) > 1:
+                st.wait_event(hev)
+            else:
+                be.dev_sha512(0, sq, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, b["hd2"].data_ptr())
             be.dev_group_and(0, sq, first.data_ptr(), cnt.data_ptr(), G, b["mbits"].data_ptr(), b["gbits"].data_ptr())
         else:
             be.dev_verify(0, sq, ntcrypto.NT_MODE_STRICT, tmp_pk.data_ptr(), hsig.data_ptr(), ids.data_ptr(),
@@ -941,7 +965,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
         barrier()
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
-        fork, join = fork_join(streams[:slots(cached)], stream)
+        fork, join = fork_join(streams[:slots(cached)] + (side if side and slots(cached) > 1 else []), stream)
         t0 = time.perf_counter()
         ev0.record(stream)
         fork(ev0)
@@ -975,7 +999,8 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
             rf["frac_one_stream_launch"] = round(ach / MAD_PEAK_TS, 4)
         progress("cfg3 %s: %.2f M certificates/s" % (key, out[key]["certs_per_s"] / 1e6))
     if world == 1 and fused and os.environ.get("NT_BENCH_SHARDS", "1") != "0":
-        out["shard_of"] = bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, stream, barrier, G, quorum,
+        out["shard_of"] = bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream, barrier, G,
+                                            quorum,
                                             dict(hdr_flat=hdr_flat, h_off=h_off, h_len=h_len, cpre=cpre, c_off=c_off,
                                                  c_len=c_len, ids=ids, vkey=vkey, hkey=hkey, vsig=vsig, hsig=hsig,
                                                  v_off=v_off, v_len=v_len, i_off=i_off, i_len=i_len, first=first,
@@ -1005,7 +1030,9 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
             **out}
 
 
-def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, stream, barrier, G, quorum, t, expect, rate1):
+def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream, barrier, G,
+                                            quorum, t, expect,
+                      rate1):
     """Config 3's 2/4/8-GPU shards rehearsed on this GPU (BASELINE configs[2] is
     strong-scaled: each of N GPUs verifies G/N certificates): the first G/N
     certificates through the same fused step (2 digests, one NT_MODE_MIXED
@@ -1050,12 +1077,20 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, stream, barri
             if timed:
                 kev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
                 kev[-1][0].record(st)
+            if side:
+                be.dev_sha512(0, side[i % nst].cuda_stream, t["hdr_flat"].data_ptr(), t["h_off"].data_ptr(),
+                              t["h_len"].data_ptr(), Gs, b["hd2"].data_ptr())
+                hev = torch.cuda.Event()
+                hev.record(side[i % nst])
             ks.dev_verify(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(),
                           m_off.data_ptr(), m_len.data_ptr(), Vs + Gs, b["mbits"].data_ptr())
             if timed:
                 kev[-1][1].record(st)
-            be.dev_sha512(0, sq, t["hdr_flat"].data_ptr(), t["h_off"].data_ptr(), t["h_len"].data_ptr(), Gs,
-                          b["hd2"].data_ptr())
+            if side:
+                st.wait_event(hev)
+            else:
+                be.dev_sha512(0, sq, t["hdr_flat"].data_ptr(), t["h_off"].data_ptr(), t["h_len"].data_ptr(), Gs,
+                              b["hd2"].data_ptr())
             be.dev_group_and(0, sq, t["first"].data_ptr(), t["cnt"].data_ptr(), Gs, b["mbits"].data_ptr(),
                              b["gbits"].data_ptr())
 
@@ -1064,7 +1099,7 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, stream, barri
         barrier()
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
-        fork, join = fork_join(streams, stream)
+        fork, join = fork_join(streams + (side or []), stream)
         t0 = time.perf_counter()
         ev0.record(stream)
         fork(ev0)

@@ -110,6 +110,7 @@ NT_D NT_INLINE bool wave_any(bool x) { return __ballot(x) != 0; }
 // round | u64 np | np x (digest 32, worker u32) | u64 nq | nq x digest 32 |
 // id 32 | signature 64 | u64 nv | nv x (u64 44 | key base64 (44) | signature 64)
 __global__ __launch_bounds__(kBlock) void k_cert_parse(CertCommittee c, CertBufs b) {
+  aux_priority();
   const uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63u;
   if (i >= b.n) return;  // whole waves
@@ -185,6 +186,7 @@ __global__ __launch_bounds__(kBlock) void k_cert_parse(CertCommittee c, CertBufs
 // exclusive scans (one workgroup): vbase[i] = sum nv[< i], pbase[i] = sum of
 // the 16-byte-rounded preimage lengths; [n] = the totals
 __global__ __launch_bounds__(1024) void k_cert_scan(CertBufs b) {
+  aux_priority();
   __shared__ uint64_t ta[1024], tb[1024];
   const uint32_t t = threadIdx.x;
   const uint64_t n = b.n, per = (n + 1023) / 1024;
@@ -223,6 +225,7 @@ __global__ __launch_bounds__(1024) void k_cert_scan(CertBufs b) {
 // SHA-512 launch); SHA-512 inputs i (header preimage) and n + i (certificate
 // preimage id || round || origin, messages.rs:226-234).
 __global__ __launch_bounds__(kBlock) void k_cert_scatter(CertCommittee c, CertBufs b) {
+  aux_priority();
   __shared__ uint32_t vkey[kWavesPerBlock][kMaxVotes];
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + w;
@@ -334,6 +337,7 @@ NT_D NT_INLINE bool word_bit(const uint64_t* w, uint64_t i) { return (w[i >> 6] 
 // author, workers and signature (:48-67), the quorum loop (:198-211), the votes'
 // verify_batch (:213); 0xff = decided by the host decoder
 __global__ __launch_bounds__(kBlock) void k_cert_verdict(CertCommittee c, CertBufs b, uint64_t gc_round) {
+  aux_priority();
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= b.n) return;
   const uint32_t fl = b.flags[i];

@@ -37,6 +37,7 @@ __global__ __launch_bounds__(kBlock) void k_sha512_trunc32(const uint8_t* __rest
                                                           const uint64_t* __restrict__ off,
                                                           const uint64_t* __restrict__ len,
                                                           uint64_t n, uint32_t* __restrict__ out) {
+  aux_priority();
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   uint64_t st[8];
@@ -85,6 +86,7 @@ __global__ __launch_bounds__(128) void k_sha512_pipe(const uint8_t* __restrict__
                                                      const uint64_t* __restrict__ off,
                                                      const uint64_t* __restrict__ len, uint64_t n,
                                                      uint32_t* __restrict__ out) {
+  aux_priority();
   __shared__ uint4 ring[2][40 * 64];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = threadIdx.x >> 6;
@@ -211,6 +213,7 @@ __global__ void k_wcomb_fill(const uint32_t* __restrict__ bases, uint32_t nkeys,
 __global__ __launch_bounds__(kBlock) void k_group_msgs(const uint64_t* __restrict__ first,
                                                       const uint32_t* __restrict__ cnt, uint64_t G,
                                                       uint64_t* __restrict__ off, uint64_t* __restrict__ len) {
+  aux_priority();
   const uint64_t g = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63u;
   if (g >= G) return;
@@ -225,6 +228,7 @@ __global__ __launch_bounds__(kBlock) void k_group_and(const uint64_t* __restrict
                                                      const uint32_t* __restrict__ cnt, uint64_t G,
                                                      const unsigned long long* __restrict__ sig_bits,
                                                      unsigned long long* __restrict__ out_bits) {
+  aux_priority();
   const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   uint32_t ok = 0;
   if (g < G) {
@@ -431,6 +435,7 @@ NT_D NT_INLINE uint32_t sort_bucket(uint32_t k, int mixed, uint32_t nkeys) {
 
 __global__ __launch_bounds__(kBlock) void k_key_hist(const uint32_t* __restrict__ key, uint64_t n, int mixed,
                                                     uint32_t nkeys, uint32_t* __restrict__ hist) {
+  aux_priority();
   __shared__ uint32_t h[kSortBuckets];
   for (uint32_t b = threadIdx.x; b <= nkeys; b += kBlock) h[b] = 0;
   __syncthreads();
@@ -458,6 +463,7 @@ __global__ __launch_bounds__(kBlock) void k_key_hist(const uint32_t* __restrict_
 __global__ __launch_bounds__(kBlock) void k_key_scatter(const uint32_t* __restrict__ key, uint64_t n, int mixed,
                                                        uint32_t nkeys, uint32_t* __restrict__ lines,
                                                        uint32_t* __restrict__ perm) {
+  aux_priority();
   __shared__ uint32_t cnt[kSortBuckets];
   __shared__ uint32_t base[kSortBuckets];
   __shared__ uint32_t part[kBlock];
@@ -505,6 +511,7 @@ __global__ __launch_bounds__(kBlock) void k_key_scatter(const uint32_t* __restri
 // verdict bytes -> 64-bit ballot words
 __global__ __launch_bounds__(kBlock) void k_pack_bytes(const uint8_t* __restrict__ b, uint64_t n,
                                                       unsigned long long* __restrict__ out) {
+  aux_priority();
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const unsigned long long bal = __ballot(i < n && b[i] != 0);
   const uint64_t wbase = i & ~(uint64_t)63;

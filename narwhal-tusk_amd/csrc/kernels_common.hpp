@@ -12,6 +12,22 @@
 namespace nt {
 
 constexpr int kBlock = 256;
+
+// Short kernels that run beside a long key-cache or verify launch of another
+// stream (digests, key sort, verdict packing, group AND, wire parsing) raise
+// their waves' issue priority on entry.  The SIMD arbiter otherwise prefers
+// the older waves of the long launch, which is VALU-issue-bound: a 15 us
+// certificate-digest launch on the next pipeline step then waits ~0.8 ms, for
+// the other launch's tail (rocprofv3 trace).  -DNT_AUX_PRIO=0
+// keeps the default priority (A/B).
+#ifndef NT_AUX_PRIO
+#define NT_AUX_PRIO 2
+#endif
+NT_D NT_INLINE void aux_priority() {
+#if NT_AUX_PRIO
+  __builtin_amdgcn_s_setprio(NT_AUX_PRIO);
+#endif
+}
 #ifndef NT_VERIFY_PER_LANE
 #define NT_VERIFY_PER_LANE 2
 #endif
