@@ -898,9 +898,10 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
         # certificate digests first (the votes' message); the header-id digests
         # (3.3 KB serial chains, latency-bound) are only needed by the verdict, so
         # they go after the signature launch, where they overlap the other stream
-        be.dev_sha512(0, sq, cpre.data_ptr(), c_off.data_ptr(), c_len.data_ptr(), G, b["cd2"].data_ptr())
+        be.dev_sha512(0, sq, cpre.data_ptr(), c_off.data_ptr(), c_len.data_ptr(), G, b["cd2"].data_ptr(), max_len=72)
         if not (cached and fused):
-            be.dev_sha512(0, sq, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, b["hd2"].data_ptr())
+            be.dev_sha512(0, sq, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, b["hd2"].data_ptr(),
+                          max_len=hlen)
         if cached and not fused:   # A/B reference: the header and vote launches separately
             ks.dev_verify(0, sq, ntcrypto.NT_MODE_STRICT, hkey.data_ptr(), hsig.data_ptr(), ids.data_ptr(),
                           i_off.data_ptr(), i_len.data_ptr(), G, b["hbits"].data_ptr())
@@ -914,7 +915,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
             if side and slots(cached) > 1:
                 # header ids beside the signature launch; the step's last kernel waits for them
                 be.dev_sha512(0, side[k].cuda_stream, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G,
-                              b["hd2"].data_ptr())
+                              b["hd2"].data_ptr(), max_len=hlen)
                 hev = torch.cuda.Event()
                 hev.record(side[k])
             ks.dev_verify(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(),
@@ -924,7 +925,8 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
             if side and slots(cached) > 1:
                 st.wait_event(hev)
             else:
-                be.dev_sha512(0, sq, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, b["hd2"].data_ptr())
+                be.dev_sha512(0, sq, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, b["hd2"].data_ptr(),
+                              max_len=hlen)
             be.dev_group_and(0, sq, first.data_ptr(), cnt.data_ptr(), G, b["mbits"].data_ptr(), b["gbits"].data_ptr())
         else:
             be.dev_verify(0, sq, ntcrypto.NT_MODE_STRICT, tmp_pk.data_ptr(), hsig.data_ptr(), ids.data_ptr(),
@@ -1001,7 +1003,8 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
     if world == 1 and fused and os.environ.get("NT_BENCH_SHARDS", "1") != "0":
         out["shard_of"] = bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream, barrier, G,
                                             quorum,
-                                            dict(hdr_flat=hdr_flat, h_off=h_off, h_len=h_len, cpre=cpre, c_off=c_off,
+                                            dict(hdr_flat=hdr_flat, h_off=h_off, h_len=h_len, hlen=hlen, cpre=cpre,
+                                                 c_off=c_off,
                                                  c_len=c_len, ids=ids, vkey=vkey, hkey=hkey, vsig=vsig, hsig=hsig,
                                                  v_off=v_off, v_len=v_len, i_off=i_off, i_len=i_len, first=first,
                                                  cnt=cnt),
@@ -1073,13 +1076,13 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream,
             sq = st.cuda_stream
             b = bufs[i % nst]
             be.dev_sha512(0, sq, t["cpre"].data_ptr(), t["c_off"].data_ptr(), t["c_len"].data_ptr(), Gs,
-                          b["msgbuf"].data_ptr())
+                          b["msgbuf"].data_ptr(), max_len=72)
             if timed:
                 kev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
                 kev[-1][0].record(st)
             if side:
                 be.dev_sha512(0, side[i % nst].cuda_stream, t["hdr_flat"].data_ptr(), t["h_off"].data_ptr(),
-                              t["h_len"].data_ptr(), Gs, b["hd2"].data_ptr())
+                              t["h_len"].data_ptr(), Gs, b["hd2"].data_ptr(), max_len=t["hlen"])
                 hev = torch.cuda.Event()
                 hev.record(side[i % nst])
             ks.dev_verify(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(),
@@ -1090,7 +1093,7 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream,
                 st.wait_event(hev)
             else:
                 be.dev_sha512(0, sq, t["hdr_flat"].data_ptr(), t["h_off"].data_ptr(), t["h_len"].data_ptr(), Gs,
-                              b["hd2"].data_ptr())
+                              b["hd2"].data_ptr(), max_len=t["hlen"])
             be.dev_group_and(0, sq, t["first"].data_ptr(), t["cnt"].data_ptr(), Gs, b["mbits"].data_ptr(),
                              b["gbits"].data_ptr())
 

@@ -107,6 +107,7 @@ struct Chunk {
   uint64_t a = 0, b = 0;     // messages [a, b) of the shard
   uint64_t base = 0, span = 0;  // host bytes [base, base + span)
   uint64_t vmax = 0;
+  uint64_t lmax = 0;  // longest message (bounds its header preimage)
   nt::CertBufs cb{};
 };
 
@@ -209,10 +210,12 @@ int ingest_front(Device& dv, IngestState& S, Side& sd, Chunk& ch, const nt_commi
   ch.base = mn & ~(uint64_t)15;
   ch.span = mx - ch.base;
   ch.vmax = 0;
+  ch.lmax = 0;
   for (uint64_t i = ch.a; i < ch.b; ++i) {
     ho[i - ch.a] = len[i] ? kSlack + off[i] - ch.base : kSlack;
     hl[i - ch.a] = len[i];
     ch.vmax += len[i] / 116;
+    ch.lmax = std::max(ch.lmax, len[i]);
   }
   NT_CHK0(grow(sd.wire, ch.span + 2 * kSlack, s));
   NT_CHK0(grow(sd.moff, m * 8, s));
@@ -283,7 +286,7 @@ int ingest_back(Device& dv, IngestState& S, Side& sd, int parity, Chunk& ch, con
   b.smlen = b.smoff + nsig;
   b.sig_words = sd.words.as<uint64_t>();
   NT_TRY(nt::launch_cert_scatter(pd.c, b, s));
-  NT_TRY(nt::launch_sha512_trunc32(b.mbase, b.soff, b.slen, 2 * m, b.mbase + 32 * m, s));
+  NT_TRY(nt::launch_sha512_trunc32(b.mbase, b.soff, b.slen, 2 * m, b.mbase + 32 * m, s, std::max<uint64_t>(ch.lmax, 72)));
   NT_CHK0(dv.ensure_stash(parity, nsig));
   void* st = parity ? dv.stash2.p : dv.d[B_STASH].p;
   void* so = parity ? dv.sort2.p : dv.d[B_SORT].p;

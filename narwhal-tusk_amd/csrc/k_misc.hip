@@ -57,6 +57,13 @@ __global__ __launch_bounds__(kBlock) void k_sha512_trunc32(const uint8_t* __rest
 // (consumer) runs the 80 rounds of block b-1 from the other slot.  One
 // s_barrier per block; the consumer's stream is ~2/3 of the one-wave stream.
 constexpr int kPipeMaxMsgs = 32768;  // 80 KB LDS per workgroup: 2 per CU
+// ... and only for long messages: when every message is known to be shorter
+// (headers, votes and certificate digests: 72 B - 3.3 KB) the one-lane kernel
+// (no LDS) runs -- a pipe launch's 80 KB workgroups can hold a CU's LDS while a
+// key-cache launch of another stream runs there, and a short digest launch
+// queued behind them then waits for that launch's tail (rocprofv3 trace,
+// DESIGN.md §10).
+constexpr uint64_t kPipeMinLen = 16384;
 struct KwLdsSink {
   uint4* slot;  // [40][64]
   uint32_t lane;
@@ -289,9 +296,9 @@ __global__ __launch_bounds__(kBlock) void k_ed25519_sign(const uint32_t* __restr
 // Launchers (host)
 // --------------------------------------------------------------------------
 hipError_t launch_sha512_trunc32(const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
-                                 uint64_t n, uint8_t* d_out32, hipStream_t s) {
+                                 uint64_t n, uint8_t* d_out32, hipStream_t s, uint64_t max_len) {
   if (n == 0) return hipSuccess;
-  if (n <= (uint64_t)kPipeMaxMsgs && !std::getenv("NT_SHA_NO_PIPE")) {
+  if (n <= (uint64_t)kPipeMaxMsgs && max_len >= kPipeMinLen && !std::getenv("NT_SHA_NO_PIPE")) {
     hipLaunchKernelGGL(k_sha512_pipe, dim3((uint32_t)((n + 63) / 64)), dim3(128), 0, s, d_data, d_off, d_len, n,
                        (uint32_t*)d_out32);
     return hipGetLastError();

@@ -653,9 +653,11 @@ int nt_sha512_trunc32(nt_ctx* ctx, const uint8_t* data, const uint64_t* off, con
       const uint64_t a = ch[c].first, b = ch[c].second;
       NT_CHK(msg_copy(dv, data, off, len, lo, ms, c, a, b));
       NT_TRY(dv.fence((int)c));
+      uint64_t ml = 0;  // the chunk's longest message selects the kernel
+      for (uint64_t i = lo + a; i < lo + b; ++i) ml = std::max(ml, len[i]);
       NT_TRY(nt::launch_sha512_trunc32(dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>() + a,
                                        dv.d[B_LEN].as<uint64_t>() + a, b - a, dv.d[B_OUT].as<uint8_t>() + 32 * a,
-                                       dv.cstr((int)c)));
+                                       dv.cstr((int)c), ml));
     }
     NT_TRY(dv.join());
     NT_TRY(hipMemcpyAsync(out32 + 32 * lo, dv.d[B_OUT].p, m * 32, hipMemcpyDeviceToHost, dv.stream));
@@ -1152,6 +1154,17 @@ int nt_dev_sha512_trunc32(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_d
   NT_TRY(hipSetDevice(dv->ordinal));
   hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
   NT_TRY(nt::launch_sha512_trunc32(d_data, d_off, d_len, n, d_out32, s));
+  return NT_OK;
+}
+
+int nt_dev_sha512_trunc32_bounded(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_data,
+                                  const uint64_t* d_off, const uint64_t* d_len, uint64_t n, uint64_t max_len,
+                                  uint8_t* d_out32) {
+  Device* dv = dev_of(ctx, dev);
+  if (!dv) return NT_EINVAL;
+  NT_TRY(hipSetDevice(dv->ordinal));
+  hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
+  NT_TRY(nt::launch_sha512_trunc32(d_data, d_off, d_len, n, d_out32, s, max_len));
   return NT_OK;
 }
 

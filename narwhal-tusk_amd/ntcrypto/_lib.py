@@ -30,6 +30,7 @@ EXPORTED = [
     "nt_init", "nt_init_device", "nt_init_devices", "nt_free", "nt_num_devices", "nt_strerror", "nt_version",
     "nt_sha512_trunc32", "nt_ed25519_verify_strict", "nt_ed25519_verify_batch_groups",
     "nt_ed25519_sign_batch", "nt_ed25519_keypair_batch", "nt_dev_sha512_trunc32",
+    "nt_dev_sha512_trunc32_bounded",
     "nt_dev_ed25519_verify", "nt_dev_group_and", "nt_dev_ed25519_sign", "nt_keyset_create",
     "nt_keyset_free", "nt_keyset_flags", "nt_keyset_info", "nt_ed25519_verify_keyset", "nt_ed25519_verify_batch_groups_keyset",
     "nt_dev_ed25519_verify_keyset", "nt_host_alloc", "nt_host_free", "nt_set_small_call_path", "nt_call_counts",
@@ -74,6 +75,7 @@ def load_library(path=None):
     lib.nt_ed25519_sign_batch.argtypes = [_vp, _u8p, _u8p, _u64p, _u64p, _u64, _u8p, _u8p]
     lib.nt_ed25519_keypair_batch.argtypes = [_vp, _u8p, _u64, _u8p]
     lib.nt_dev_sha512_trunc32.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, _u64, _vp]
+    lib.nt_dev_sha512_trunc32_bounded.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, _u64, _u64, _vp]
     lib.nt_dev_ed25519_verify.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_int, _vp, _vp, _vp, _vp, _vp,
                                           _u64, _vp]
     lib.nt_dev_group_and.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _u64, _vp, _vp]
@@ -295,9 +297,15 @@ class Backend:
         _check(self.lib.nt_dev_ed25519_verify(self.ctx, dev, stream, mode, d_pk, d_sig, d_msg, d_off, d_len,
                                               n, d_out), "nt_dev_ed25519_verify")
 
-    def dev_sha512(self, dev, stream, d_data, d_off, d_len, n, d_out):
-        _check(self.lib.nt_dev_sha512_trunc32(self.ctx, dev, stream, d_data, d_off, d_len, n, d_out),
-               "nt_dev_sha512_trunc32")
+    def dev_sha512(self, dev, stream, d_data, d_off, d_len, n, d_out, max_len=None):
+        """max_len: an upper bound of the message lengths, if known (selects the
+        kernel: nt_dev_sha512_trunc32_bounded)"""
+        if max_len is None:
+            _check(self.lib.nt_dev_sha512_trunc32(self.ctx, dev, stream, d_data, d_off, d_len, n, d_out),
+                   "nt_dev_sha512_trunc32")
+        else:
+            _check(self.lib.nt_dev_sha512_trunc32_bounded(self.ctx, dev, stream, d_data, d_off, d_len, n,
+                                                          int(max_len), d_out), "nt_dev_sha512_trunc32_bounded")
 
     def dev_sign(self, dev, stream, d_seed, d_msg, d_off, d_len, n, d_pk, d_sig):
         _check(self.lib.nt_dev_ed25519_sign(self.ctx, dev, stream, d_seed, d_msg, d_off, d_len, n, d_pk, d_sig),

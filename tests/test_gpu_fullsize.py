@@ -179,3 +179,32 @@ def test_random_corruptions_vs_oracle_200k(env, oracle):
     bad = np.nonzero(got != want)[0]
     assert len(bad) == 0, [(int(i), int(kind[i])) for i in bad[:20]]
     assert want[kind <= 2].all() and not want[(kind >= 4) & (kind <= 8)].any()
+
+
+def test_sha512_bounded_hint_selects_kernel_not_result(env):
+    """nt_dev_sha512_trunc32_bounded: max_len only selects the kernel (one-lane
+    below 16 KB, the two-wave pipe above, for launches of <= 32,768 messages):
+    digests equal hashlib whatever the hint says -- a right bound, a bound
+    below some lengths (a wrong hint) and no hint -- over lengths around every
+    padding edge and across the 16 KB switch."""
+    torch, be, dev, sp = env.torch, env.be, env.dev, env.sp
+    rng = np.random.default_rng(16)
+    lens = [0, 1, 72, 111, 112, 127, 128, 129, 239, 240, 3336, 16383, 16384, 16385, 40000]
+    lens += rng.integers(0, 20000, 200).tolist()
+    off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    blob = rng.integers(0, 256, int(sum(lens)) + 64, dtype=np.uint8)
+    want = [hashlib.sha512(blob[o:o + n].tobytes()).digest()[:32] for o, n in zip(off, lens)]
+    n = len(lens)
+    with torch.cuda.stream(env.stream):
+        d = torch.from_numpy(blob).to(dev)
+        o = torch.from_numpy(off).to(dev)
+        ln = torch.tensor(lens, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    for hint in (None, max(lens), 4096, 72):
+        out = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
+        be.dev_sha512(0, sp, d.data_ptr(), o.data_ptr(), ln.data_ptr(), n, out.data_ptr(), max_len=hint)
+        torch.cuda.synchronize(dev)
+        got = out.cpu().numpy()
+        bad = [i for i in range(n) if got[i].tobytes() != want[i]]
+        assert not bad, (hint, bad[:5])
