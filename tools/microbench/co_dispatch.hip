@@ -8,7 +8,9 @@
 // registers per lane.  `tiny`: 49 workgroups of 256 threads, a short VALU loop,
 // optionally at wave priority PRIO (s_setprio).  Printed: tiny's duration
 // alone and when enqueued 1 ms into busy (HIP events on tiny's own stream),
-// for NV = 24 / 100 and PRIO = 0 / 2 / 3.  Every loop is bounded.
+// for NV = 24 / 100 and PRIO = 0 / 2 / 3; then the same with a busy kernel that
+// streams random 128-byte table lines (like the key-cache launch) and a tiny
+// kernel that reads its 72-80-byte messages first.  Every loop is bounded.
 // Build: hipcc -O3 --offload-arch=gfx950 co_dispatch.hip -o co_dispatch
 #include <hip/hip_runtime.h>
 
@@ -39,6 +41,36 @@ __global__ __launch_bounds__(256, 2) void busy(uint32_t* out, uint32_t iters) {
 #pragma unroll
   for (int i = 0; i < NV; ++i) s ^= v[i];
   out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+// busy_mem: like the key-cache launch -- random 128-byte line reads from a
+// large table (8 x 16 B per lane per step) between VALU work
+__global__ __launch_bounds__(256, 2) void busy_mem(const uint4* __restrict__ tab, uint64_t lines, uint32_t* out,
+                                                   uint32_t iters) {
+  uint32_t x = blockIdx.x * 256 + threadIdx.x, acc = x;
+  for (uint32_t it = 0; it < iters; ++it) {
+    x = x * 1664525u + 1013904223u;
+    const uint4* e = tab + (uint64_t)(x % (uint32_t)lines) * 8;
+    uint4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = e[i];
+#pragma unroll
+    for (int r = 0; r < 40; ++r) acc = acc * 0x9E3779B1u + (r & 1 ? v[r & 7].x : v[r & 7].w);
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+// tiny_mem: per lane a 72-byte message read (5 x 16 B) and a short VALU chain,
+// like a certificate-digest launch
+template <int PRIO>
+__global__ __launch_bounds__(256) void tiny_mem(const uint4* __restrict__ msg, uint32_t* out, uint32_t iters) {
+  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  uint32_t x = i;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) x ^= msg[(uint64_t)i * 5 + k].x;
+  for (uint32_t it = 0; it < iters; ++it) x = x * 0x9E3779B1u + it;
+  out[i] = x;
 }
 
 template <int PRIO>
@@ -82,6 +114,37 @@ static int run(hipStream_t sa, hipStream_t sb, uint32_t* d_busy, uint32_t* d_tin
   return 0;
 }
 
+template <int PRIO>
+static int run_mem(hipStream_t sa, hipStream_t sb, const uint4* tab, uint64_t lines, const uint4* msg,
+                   uint32_t* d_busy, uint32_t* d_tiny, uint32_t busy_iters, uint32_t tiny_iters, int cus) {
+  hipEvent_t e0, e1, b0, b1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventCreate(&b0));
+  CK(hipEventCreate(&b1));
+  CK(hipEventRecord(e0, sb));
+  hipLaunchKernelGGL(tiny_mem<PRIO>, dim3(49), dim3(256), 0, sb, msg, d_tiny, tiny_iters);
+  CK(hipEventRecord(e1, sb));
+  CK(hipStreamSynchronize(sb));
+  float alone = 0;
+  CK(hipEventElapsedTime(&alone, e0, e1));
+  CK(hipEventRecord(b0, sa));
+  hipLaunchKernelGGL(busy_mem, dim3(2 * cus), dim3(256), 0, sa, tab, lines, d_busy, busy_iters);
+  CK(hipEventRecord(b1, sa));
+  std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  CK(hipEventRecord(e0, sb));
+  hipLaunchKernelGGL(tiny_mem<PRIO>, dim3(49), dim3(256), 0, sb, msg, d_tiny, tiny_iters);
+  CK(hipEventRecord(e1, sb));
+  CK(hipDeviceSynchronize());
+  float beside = 0, busy_ms = 0, tiny_start = 0;
+  CK(hipEventElapsedTime(&beside, e0, e1));
+  CK(hipEventElapsedTime(&busy_ms, b0, b1));
+  CK(hipEventElapsedTime(&tiny_start, b0, e0));
+  std::printf("memory-bound busy, prio %d: tiny_mem alone %8.1f us | beside busy %8.1f us (enqueued %.2f ms into a "
+              "%.2f ms busy launch)\n", PRIO, alone * 1e3, beside * 1e3, tiny_start, busy_ms);
+  return 0;
+}
+
 int main() {
   hipDeviceProp_t p;
   CK(hipGetDeviceProperties(&p, 0));
@@ -102,6 +165,18 @@ int main() {
   if (run<100, 0>(sa, sb, d_busy, d_tiny, busy_iters / 4, tiny_iters, cus)) return 1;
   if (run<100, 2>(sa, sb, d_busy, d_tiny, busy_iters / 4, tiny_iters, cus)) return 1;
   if (run<100, 3>(sa, sb, d_busy, d_tiny, busy_iters / 4, tiny_iters, cus)) return 1;
+  // a 4 GB table of 128-byte lines, 49 x 256 messages of 80 bytes
+  const uint64_t lines = (4ull << 30) / 128;
+  uint4 *tab = nullptr, *msg = nullptr;
+  CK(hipMalloc(&tab, lines * 128));
+  CK(hipMemset(tab, 1, lines * 128));
+  CK(hipMalloc(&msg, (size_t)49 * 256 * 80));
+  CK(hipMemset(msg, 2, (size_t)49 * 256 * 80));
+  CK(hipDeviceSynchronize());
+  if (run_mem<0>(sa, sb, tab, lines, msg, d_busy, d_tiny, 4000, tiny_iters, cus)) return 1;
+  if (run_mem<2>(sa, sb, tab, lines, msg, d_busy, d_tiny, 4000, tiny_iters, cus)) return 1;
+  CK(hipFree(tab));
+  CK(hipFree(msg));
   CK(hipFree(d_busy));
   CK(hipFree(d_tiny));
   return 0;
