@@ -184,6 +184,12 @@ def side_streams(torch, dev, n):
     return [torch.cuda.Stream(dev, priority=pr) for _ in range(n)]
 
 
+# wave issue priority of the config-3 digest launches (nt_dev_sha512_trunc32_bounded):
+# the certificate digests gate the next key-cache launch (highest), the header ids
+# on the side streams do not (lowest; their queue's priority already lifts them)
+CSHA_PRIO = int(os.environ.get("NT_BENCH_CSHA_PRIO", "3"))
+HSHA_PRIO = int(os.environ.get("NT_BENCH_HSHA_PRIO", "0"))
+
 _T0 = time.time()
 
 
@@ -922,7 +928,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
         # certificate digests first (the votes' message); the header-id digests
         # (3.3 KB serial chains, latency-bound) are only needed by the verdict, so
         # they go after the signature launch, where they overlap the other stream
-        be.dev_sha512(0, sq, cpre.data_ptr(), c_off.data_ptr(), c_len.data_ptr(), G, b["cd2"].data_ptr(), max_len=72)
+        be.dev_sha512(0, sq, cpre.data_ptr(), c_off.data_ptr(), c_len.data_ptr(), G, b["cd2"].data_ptr(), max_len=72, prio=CSHA_PRIO)
         if not (cached and fused):
             be.dev_sha512(0, sq, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, b["hd2"].data_ptr(),
                           max_len=hlen)
@@ -939,7 +945,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
             if side and slots(cached) > 1:
                 # header ids beside the signature launch; the step's last kernel waits for them
                 be.dev_sha512(0, side[k].cuda_stream, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G,
-                              b["hd2"].data_ptr(), max_len=hlen)
+                              b["hd2"].data_ptr(), max_len=hlen, prio=HSHA_PRIO)
                 hev = torch.cuda.Event()
                 hev.record(side[k])
             ks.dev_verify(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(),
@@ -1100,13 +1106,13 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream,
             sq = st.cuda_stream
             b = bufs[i % nst]
             be.dev_sha512(0, sq, t["cpre"].data_ptr(), t["c_off"].data_ptr(), t["c_len"].data_ptr(), Gs,
-                          b["msgbuf"].data_ptr(), max_len=72)
+                          b["msgbuf"].data_ptr(), max_len=72, prio=CSHA_PRIO)
             if timed:
                 kev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
                 kev[-1][0].record(st)
             if side:
                 be.dev_sha512(0, side[i % nst].cuda_stream, t["hdr_flat"].data_ptr(), t["h_off"].data_ptr(),
-                              t["h_len"].data_ptr(), Gs, b["hd2"].data_ptr(), max_len=t["hlen"])
+                              t["h_len"].data_ptr(), Gs, b["hd2"].data_ptr(), max_len=t["hlen"], prio=HSHA_PRIO)
                 hev = torch.cuda.Event()
                 hev.record(side[i % nst])
             ks.dev_verify(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(),

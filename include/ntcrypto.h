@@ -279,10 +279,12 @@ int nt_dev_sha512_trunc32(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_d
  * (headers, votes, certificate digests): max_len only selects the kernel --
  * below 16 KB the one-lane kernel, which holds no LDS, so it never waits
  * behind a key-cache launch of another stream.  Any length is
- * still hashed correctly whatever max_len says. */
+ * still hashed correctly whatever max_len says.  prio: the launch's wave issue
+ * priority, 0..3 (-1 = the default, 2): a digest launch that a pipeline waits
+ * on beside long launches goes first at 3; one off the critical path at 0. */
 int nt_dev_sha512_trunc32_bounded(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_data,
                                   const uint64_t *d_off, const uint64_t *d_len, uint64_t n,
-                                  uint64_t max_len, uint8_t *d_out32);
+                                  uint64_t max_len, int prio, uint8_t *d_out32);
 /* d_out_words: ceil(n/64) little-endian 64-bit bitmap words.  Successive calls
  * alternate between the device entry's two [k]A workspaces (each ordered by
  * its own event), so batches enqueued back to back on two different streams

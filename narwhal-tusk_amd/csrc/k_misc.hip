@@ -36,8 +36,8 @@ namespace nt {
 __global__ __launch_bounds__(kBlock) void k_sha512_trunc32(const uint8_t* __restrict__ data,
                                                           const uint64_t* __restrict__ off,
                                                           const uint64_t* __restrict__ len,
-                                                          uint64_t n, uint32_t* __restrict__ out) {
-  aux_priority();
+                                                          uint64_t n, uint32_t* __restrict__ out, int prio) {
+  wave_priority(prio);
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   uint64_t st[8];
@@ -92,8 +92,8 @@ struct KwPrefetchSource {
 __global__ __launch_bounds__(128) void k_sha512_pipe(const uint8_t* __restrict__ data,
                                                      const uint64_t* __restrict__ off,
                                                      const uint64_t* __restrict__ len, uint64_t n,
-                                                     uint32_t* __restrict__ out) {
-  aux_priority();
+                                                     uint32_t* __restrict__ out, int prio) {
+  wave_priority(prio);
   __shared__ uint4 ring[2][40 * 64];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = threadIdx.x >> 6;
@@ -296,16 +296,16 @@ __global__ __launch_bounds__(kBlock) void k_ed25519_sign(const uint32_t* __restr
 // Launchers (host)
 // --------------------------------------------------------------------------
 hipError_t launch_sha512_trunc32(const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
-                                 uint64_t n, uint8_t* d_out32, hipStream_t s, uint64_t max_len) {
+                                 uint64_t n, uint8_t* d_out32, hipStream_t s, uint64_t max_len, int prio) {
   if (n == 0) return hipSuccess;
   if (n <= (uint64_t)kPipeMaxMsgs && max_len >= kPipeMinLen && !std::getenv("NT_SHA_NO_PIPE")) {
     hipLaunchKernelGGL(k_sha512_pipe, dim3((uint32_t)((n + 63) / 64)), dim3(128), 0, s, d_data, d_off, d_len, n,
-                       (uint32_t*)d_out32);
+                       (uint32_t*)d_out32, prio);
     return hipGetLastError();
   }
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_sha512_trunc32, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_data, d_off,
-                     d_len, n, (uint32_t*)d_out32);
+                     d_len, n, (uint32_t*)d_out32, prio);
   return hipGetLastError();
 }
 

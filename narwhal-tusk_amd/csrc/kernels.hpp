@@ -10,9 +10,11 @@
 namespace nt {
 
 // max_len: an upper bound of the messages' lengths when the caller knows one
-// (it selects the kernel; any length is still hashed correctly)
+// (it selects the kernel; any length is still hashed correctly); prio: wave
+// issue priority 0..3 of the launch, < 0 = the build default (NT_AUX_PRIO)
 hipError_t launch_sha512_trunc32(const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
-                                 uint64_t n, uint8_t* d_out32, hipStream_t s, uint64_t max_len = ~0ull);
+                                 uint64_t n, uint8_t* d_out32, hipStream_t s, uint64_t max_len = ~0ull,
+                                 int prio = -1);
 hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
                          const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
                          const uint32_t* d_combB, int bbits, void* d_ws, uint32_t ws_slots, uint64_t* d_out_words,

@@ -28,6 +28,14 @@ NT_D NT_INLINE void aux_priority() {
   __builtin_amdgcn_s_setprio(NT_AUX_PRIO);
 #endif
 }
+// a launch-time priority (the digest launches: nt_dev_sha512_trunc32_bounded);
+// < 0 = the build's default above
+NT_D NT_INLINE void wave_priority(int p) {
+  if (p < 0) aux_priority();
+  else if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p >= 3) __builtin_amdgcn_s_setprio(3);
+}
 #ifndef NT_VERIFY_PER_LANE
 #define NT_VERIFY_PER_LANE 2
 #endif

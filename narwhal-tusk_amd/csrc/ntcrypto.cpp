@@ -1159,12 +1159,12 @@ int nt_dev_sha512_trunc32(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_d
 
 int nt_dev_sha512_trunc32_bounded(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_data,
                                   const uint64_t* d_off, const uint64_t* d_len, uint64_t n, uint64_t max_len,
-                                  uint8_t* d_out32) {
+                                  int prio, uint8_t* d_out32) {
   Device* dv = dev_of(ctx, dev);
-  if (!dv) return NT_EINVAL;
+  if (!dv || prio > 3) return NT_EINVAL;
   NT_TRY(hipSetDevice(dv->ordinal));
   hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
-  NT_TRY(nt::launch_sha512_trunc32(d_data, d_off, d_len, n, d_out32, s, max_len));
+  NT_TRY(nt::launch_sha512_trunc32(d_data, d_off, d_len, n, d_out32, s, max_len, prio));
   return NT_OK;
 }
 

@@ -75,7 +75,8 @@ def load_library(path=None):
     lib.nt_ed25519_sign_batch.argtypes = [_vp, _u8p, _u8p, _u64p, _u64p, _u64, _u8p, _u8p]
     lib.nt_ed25519_keypair_batch.argtypes = [_vp, _u8p, _u64, _u8p]
     lib.nt_dev_sha512_trunc32.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, _u64, _vp]
-    lib.nt_dev_sha512_trunc32_bounded.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, _u64, _u64, _vp]
+    lib.nt_dev_sha512_trunc32_bounded.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, _u64, _u64, ctypes.c_int,
+                                                  _vp]
     lib.nt_dev_ed25519_verify.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_int, _vp, _vp, _vp, _vp, _vp,
                                           _u64, _vp]
     lib.nt_dev_group_and.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _u64, _vp, _vp]
@@ -297,15 +298,16 @@ class Backend:
         _check(self.lib.nt_dev_ed25519_verify(self.ctx, dev, stream, mode, d_pk, d_sig, d_msg, d_off, d_len,
                                               n, d_out), "nt_dev_ed25519_verify")
 
-    def dev_sha512(self, dev, stream, d_data, d_off, d_len, n, d_out, max_len=None):
+    def dev_sha512(self, dev, stream, d_data, d_off, d_len, n, d_out, max_len=None, prio=None):
         """max_len: an upper bound of the message lengths, if known (selects the
-        kernel: nt_dev_sha512_trunc32_bounded)"""
-        if max_len is None:
+        kernel); prio: wave issue priority 0..3 (nt_dev_sha512_trunc32_bounded)"""
+        if max_len is None and prio is None:
             _check(self.lib.nt_dev_sha512_trunc32(self.ctx, dev, stream, d_data, d_off, d_len, n, d_out),
                    "nt_dev_sha512_trunc32")
         else:
-            _check(self.lib.nt_dev_sha512_trunc32_bounded(self.ctx, dev, stream, d_data, d_off, d_len, n,
-                                                          int(max_len), d_out), "nt_dev_sha512_trunc32_bounded")
+            _check(self.lib.nt_dev_sha512_trunc32_bounded(
+                self.ctx, dev, stream, d_data, d_off, d_len, n, (1 << 64) - 1 if max_len is None else int(max_len),
+                -1 if prio is None else int(prio), d_out), "nt_dev_sha512_trunc32_bounded")
 
     def dev_sign(self, dev, stream, d_seed, d_msg, d_off, d_len, n, d_pk, d_sig):
         _check(self.lib.nt_dev_ed25519_sign(self.ctx, dev, stream, d_seed, d_msg, d_off, d_len, n, d_pk, d_sig),

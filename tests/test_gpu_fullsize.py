@@ -185,8 +185,8 @@ def test_sha512_bounded_hint_selects_kernel_not_result(env):
     """nt_dev_sha512_trunc32_bounded: max_len only selects the kernel (one-lane
     below 16 KB, the two-wave pipe above, for launches of <= 32,768 messages):
     digests equal hashlib whatever the hint says -- a right bound, a bound
-    below some lengths (a wrong hint) and no hint -- over lengths around every
-    padding edge and across the 16 KB switch."""
+    below some lengths (a wrong hint) and no hint, at wave priorities 0..3 --
+    over lengths around every padding edge and across the 16 KB switch."""
     torch, be, dev, sp = env.torch, env.be, env.dev, env.sp
     rng = np.random.default_rng(16)
     lens = [0, 1, 72, 111, 112, 127, 128, 129, 239, 240, 3336, 16383, 16384, 16385, 40000]
@@ -200,10 +200,10 @@ def test_sha512_bounded_hint_selects_kernel_not_result(env):
         o = torch.from_numpy(off).to(dev)
         ln = torch.tensor(lens, dtype=torch.int64, device=dev)
     torch.cuda.synchronize(dev)
-    for hint in (None, max(lens), 4096, 72):
+    for hint, prio in ((None, None), (max(lens), None), (4096, 3), (72, 0), (None, 1)):
         out = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
         torch.cuda.synchronize(dev)
-        be.dev_sha512(0, sp, d.data_ptr(), o.data_ptr(), ln.data_ptr(), n, out.data_ptr(), max_len=hint)
+        be.dev_sha512(0, sp, d.data_ptr(), o.data_ptr(), ln.data_ptr(), n, out.data_ptr(), max_len=hint, prio=prio)
         torch.cuda.synchronize(dev)
         got = out.cpu().numpy()
         bad = [i for i in range(n) if got[i].tobytes() != want[i]]
