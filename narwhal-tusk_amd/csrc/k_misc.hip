@@ -33,11 +33,8 @@ namespace nt {
 // --------------------------------------------------------------------------
 // SHA-512 digests
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_sha512_trunc32(const uint8_t* __restrict__ data,
-                                                          const uint64_t* __restrict__ off,
-                                                          const uint64_t* __restrict__ len,
-                                                          uint64_t n, uint32_t* __restrict__ out, int prio) {
-  wave_priority(prio);
+NT_D NT_INLINE void sha512_trunc32_one(const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+                                       const uint64_t* __restrict__ len, uint64_t n, uint32_t* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   uint64_t st[8];
@@ -47,6 +44,25 @@ __global__ __launch_bounds__(kBlock) void k_sha512_trunc32(const uint8_t* __rest
   uint4* o = (uint4*)(out + 8 * i);
   o[0] = make_uint4(w[0], w[1], w[2], w[3]);
   o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+__global__ __launch_bounds__(kBlock) void k_sha512_trunc32(const uint8_t* __restrict__ data,
+                                                          const uint64_t* __restrict__ off,
+                                                          const uint64_t* __restrict__ len,
+                                                          uint64_t n, uint32_t* __restrict__ out, int prio) {
+  wave_priority(prio);
+  sha512_trunc32_one(data, off, len, n, out);
+}
+// The same for short messages (<= kLeanMaxLen bytes: certificate / vote
+// digests) in at most 64 VGPRs (8 waves per SIMD; the compression spills a
+// little): beside two co-resident key-cache launches (4 x 112 VGPRs per SIMD)
+// only 64 are free, and a launch that needs more waits for one of them to end
+// (tools/microbench/co_dispatch.hip).
+__global__ __launch_bounds__(kBlock, 8) void k_sha512_trunc32_lean(const uint8_t* __restrict__ data,
+                                                                   const uint64_t* __restrict__ off,
+                                                                   const uint64_t* __restrict__ len,
+                                                                   uint64_t n, uint32_t* __restrict__ out, int prio) {
+  wave_priority(prio);
+  sha512_trunc32_one(data, off, len, n, out);
 }
 
 // Few long messages (n <= kPipeMaxMsgs, e.g. config 4: 16,384 x 500 kB): one
@@ -64,6 +80,10 @@ constexpr int kPipeMaxMsgs = 32768;  // 80 KB LDS per workgroup: 2 per CU
 // queued behind them then waits for that launch's tail (rocprofv3 trace,
 // DESIGN.md §10).
 constexpr uint64_t kPipeMinLen = 16384;
+#ifndef NT_SHA_LEAN_MAX
+#define NT_SHA_LEAN_MAX 256
+#endif
+constexpr uint64_t kLeanMaxLen = NT_SHA_LEAN_MAX;  // 0 disables the lean kernel (A/B)
 struct KwLdsSink {
   uint4* slot;  // [40][64]
   uint32_t lane;
@@ -304,8 +324,12 @@ hipError_t launch_sha512_trunc32(const uint8_t* d_data, const uint64_t* d_off, c
     return hipGetLastError();
   }
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_sha512_trunc32, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_data, d_off,
-                     d_len, n, (uint32_t*)d_out32, prio);
+  if (max_len <= kLeanMaxLen)
+    hipLaunchKernelGGL(k_sha512_trunc32_lean, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_data, d_off, d_len, n,
+                       (uint32_t*)d_out32, prio);
+  else
+    hipLaunchKernelGGL(k_sha512_trunc32, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_data, d_off,
+                       d_len, n, (uint32_t*)d_out32, prio);
   return hipGetLastError();
 }
 

@@ -57,7 +57,9 @@ def test_two_rank_bench_on_one_gpu():
     lines = [json.loads(x) for x in re.findall(r"^\{.*\}$", r.stdout, re.M)]
     assert len(lines) == 1
     d = lines[0]
-    assert d["n_gpus"] == 2 and d["parity"] == {"mismatches_vs_expected": 0, "checked": 2 * 8192}
+    # both config-2 runs checked on both ranks: the pipelined headline and the one-stream figure
+    assert d["n_gpus"] == 2 and d["parity"] == {"mismatches_vs_expected": 0, "checked": 2 * 2 * 8192}
+    assert d["streams"] == 2 and d["one_stream"]["value"] > 0
     assert d["certificates"]["keyset"]["mismatches_vs_expected"] == 0
     assert d["sha512"]["spot_check_ok"]
     # the whole metric near the front of the line, and every

@@ -73,6 +73,24 @@ __global__ __launch_bounds__(256) void tiny_mem(const uint4* __restrict__ msg, u
   out[i] = x;
 }
 
+// tiny_wide: the tiny loop holding NT live registers per lane (~2 NT VGPRs,
+// like a digest launch's 84)
+template <int PRIO, int NT>
+__global__ __launch_bounds__(256) void tiny_wide(uint32_t* out, uint32_t iters) {
+  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
+  uint32_t v[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) v[i] = threadIdx.x + (uint32_t)i;
+  for (uint32_t it = 0; it < iters / 16; ++it) {
+#pragma unroll
+    for (int i = 0; i < NT; ++i) v[i] = v[i] * 0x9E3779B1u + v[(i + 1) % NT];
+  }
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < NT; ++i) s ^= v[i];
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
 template <int PRIO>
 __global__ __launch_bounds__(256) void tiny(uint32_t* out, uint32_t iters) {
   if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
@@ -145,6 +163,39 @@ static int run_mem(hipStream_t sa, hipStream_t sb, const uint4* tab, uint64_t li
   return 0;
 }
 
+// tiny_wide beside one or two co-resident busy<NV> launches (2 waves per SIMD each)
+template <int NV, int PRIO, int NT>
+static int run_wide(hipStream_t sa, hipStream_t sa2, hipStream_t sb, uint32_t* d_busy, uint32_t* d_busy2,
+                    uint32_t* d_tiny, uint32_t busy_iters, uint32_t tiny_iters, int cus, int nbusy) {
+  hipEvent_t e0, e1, b0, b1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventCreate(&b0));
+  CK(hipEventCreate(&b1));
+  CK(hipEventRecord(e0, sb));
+  hipLaunchKernelGGL((tiny_wide<PRIO, NT>), dim3(49), dim3(256), 0, sb, d_tiny, tiny_iters);
+  CK(hipEventRecord(e1, sb));
+  CK(hipStreamSynchronize(sb));
+  float alone = 0;
+  CK(hipEventElapsedTime(&alone, e0, e1));
+  CK(hipEventRecord(b0, sa));
+  hipLaunchKernelGGL(busy<NV>, dim3(2 * cus), dim3(256), 0, sa, d_busy, busy_iters);
+  if (nbusy > 1) hipLaunchKernelGGL(busy<NV>, dim3(2 * cus), dim3(256), 0, sa2, d_busy2, busy_iters);
+  CK(hipEventRecord(b1, sa));
+  std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  CK(hipEventRecord(e0, sb));
+  hipLaunchKernelGGL((tiny_wide<PRIO, NT>), dim3(49), dim3(256), 0, sb, d_tiny, tiny_iters);
+  CK(hipEventRecord(e1, sb));
+  CK(hipDeviceSynchronize());
+  float beside = 0, busy_ms = 0, tiny_start = 0;
+  CK(hipEventElapsedTime(&beside, e0, e1));
+  CK(hipEventElapsedTime(&busy_ms, b0, b1));
+  CK(hipEventElapsedTime(&tiny_start, b0, e0));
+  std::printf("%d x busy<%d>, tiny_wide<%d> prio %d: alone %8.1f us | beside %8.1f us (enqueued %.2f ms into a "
+              "%.2f ms busy launch)\n", nbusy, NV, NT, PRIO, alone * 1e3, beside * 1e3, tiny_start, busy_ms);
+  return 0;
+}
+
 int main() {
   hipDeviceProp_t p;
   CK(hipGetDeviceProperties(&p, 0));
@@ -165,6 +216,17 @@ int main() {
   if (run<100, 0>(sa, sb, d_busy, d_tiny, busy_iters / 4, tiny_iters, cus)) return 1;
   if (run<100, 2>(sa, sb, d_busy, d_tiny, busy_iters / 4, tiny_iters, cus)) return 1;
   if (run<100, 3>(sa, sb, d_busy, d_tiny, busy_iters / 4, tiny_iters, cus)) return 1;
+  {
+    hipStream_t sa2;
+    uint32_t* d_busy2 = nullptr;
+    CK(hipStreamCreateWithFlags(&sa2, hipStreamNonBlocking));
+    CK(hipMalloc(&d_busy2, (size_t)2 * cus * 256 * 4));
+    if (run_wide<53, 2, 40>(sa, sa2, sb, d_busy, d_busy2, d_tiny, busy_iters / 2, tiny_iters, cus, 1)) return 1;
+    if (run_wide<53, 2, 40>(sa, sa2, sb, d_busy, d_busy2, d_tiny, busy_iters / 2, tiny_iters, cus, 2)) return 1;
+    if (run_wide<53, 0, 40>(sa, sa2, sb, d_busy, d_busy2, d_tiny, busy_iters / 2, tiny_iters, cus, 1)) return 1;
+    if (run_wide<53, 2, 2>(sa, sa2, sb, d_busy, d_busy2, d_tiny, busy_iters / 2, tiny_iters, cus, 2)) return 1;
+    CK(hipFree(d_busy2));
+  }
   // a 4 GB table of 128-byte lines, 49 x 256 messages of 80 bytes
   const uint64_t lines = (4ull << 30) / 128;
   uint4 *tab = nullptr, *msg = nullptr;
