@@ -437,6 +437,10 @@ def main():
             # covers its neighbour's tail)
             line["one_stream"] = {"value": line["value"], "ms_per_step": line["ms_per_step"],
                                   "note": "the same steps strictly back to back on one stream"}
+            line["roofline"]["kernel_ms_note"] = (
+                "per-launch duration from the one_stream timed region (HIP events around each launch on its "
+                "stream); in the pipelined region a launch's span covers its neighbour's tail, so the "
+                "kernel's own time is taken where launches do not overlap")
             line["value"] = ts["verifies_per_s"]
             line["ms_per_step"] = ts["ms_per_step"]
             line["streams"] = 2
