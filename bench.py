@@ -1082,9 +1082,13 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream,
     aggregate this GPU's shard rate implies (the 8-GPU run itself is the
     driver's)."""
     res = {}
-    steps = max(1, min(args.steps, 10))
+    base = max(1, min(args.steps, 10))   # the 1-GPU keyset run's step count
     nst = len(streams)
     for N in (2, 4, 8):
+        # N x as many steps as the 1-GPU run: every timed region covers the same
+        # certificates, so the two-stream pipeline's fill and drain weigh the same
+        # in the shard's rate as in the 1-GPU rate it is divided by
+        steps = base * N if os.environ.get("NT_BENCH_SHARD_EQUAL", "1") != "0" else base
         Gs = G // N
         Vs = Gs * quorum
         mkey = torch.cat([t["vkey"][:Vs], t["hkey"][:Gs] + torch.iinfo(torch.int32).min]).contiguous()
@@ -1154,7 +1158,8 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream,
             idok = (b["hd2"] == t["ids"][:Gs]).all(dim=1).cpu().numpy()
             bad += int(((gb & hb & idok) != expect[:Gs]).sum())
         rate = Gs * steps / wall
-        res[str(N)] = {"certificates": Gs, "signatures_per_launch": Vs + Gs, "certs_per_s": round(rate, 1),
+        res[str(N)] = {"certificates": Gs, "signatures_per_launch": Vs + Gs, "steps": steps,
+                       "certs_per_s": round(rate, 1),
                        "ms_per_step": round(wall * 1e3 / steps, 3),
                        "gpu_ms_per_step": round(ev0.elapsed_time(ev1) / steps, 3),
                        "keyset_launch_ms": round(float(np.mean([a.elapsed_time(b) for a, b in kev])), 3),
