@@ -988,9 +988,9 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
     runs = [("keyset", True, nst)] + ([("keyset_one_stream", True, 1)] if nst > 1 and fused else []) + \
         [("uncached", False, 1)]
     for key, cached, ns in runs:
-        # up to 10 pipelined key-cache steps (a 2-stream pipeline's fill and drain are
+        # up to 20 pipelined key-cache steps (a 2-stream pipeline's fill and drain are
         # one step each); the uncached reference (~70 ms per step) keeps 5
-        steps = max(1, min(args.steps, 10 if cached else 5))
+        steps = max(1, min(args.steps, 20 if cached else 5))
         mode_streams[cached] = ns
         kev.clear()
         # the inputs and buffers were written on `stream`: the pipeline streams
@@ -1082,13 +1082,11 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream,
     aggregate this GPU's shard rate implies (the 8-GPU run itself is the
     driver's)."""
     res = {}
-    base = max(1, min(args.steps, 10))   # the 1-GPU keyset run's step count
+    # the 1-GPU keyset run's step count: the two-stream pipeline's fill (the first
+    # step runs without a neighbour) then weighs the same in both rates
+    steps = max(1, min(args.steps, 20))
     nst = len(streams)
     for N in (2, 4, 8):
-        # N x as many steps as the 1-GPU run: every timed region covers the same
-        # certificates, so the two-stream pipeline's fill and drain weigh the same
-        # in the shard's rate as in the 1-GPU rate it is divided by
-        steps = base * N if os.environ.get("NT_BENCH_SHARD_EQUAL", "1") != "0" else base
         Gs = G // N
         Vs = Gs * quorum
         mkey = torch.cat([t["vkey"][:Vs], t["hkey"][:Gs] + torch.iinfo(torch.int32).min]).contiguous()
