@@ -44,6 +44,12 @@ import time
 
 import numpy as np
 
+
+def nbytes(t):
+    """byte size of a device tensor: the msg_bytes argument of the nt_dev_* entry points"""
+    return int(t.numel()) * int(t.element_size())
+
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "narwhal-tusk_amd"))
 
@@ -139,15 +145,15 @@ def full_host(rate, threads, host):
 
 
 def pipeline_streams(torch, be, dev, stream, n):
-    """The n streams consecutive steps alternate between: `stream` and n - 1
-    more torch streams (each on a hardware queue HIP picks).
-    NT_BENCH_LIB_STREAMS=1 (A/B): the library's two compute streams
-    (nt_dev_stream) -- measured 3-5 % slower for the same launches, one stream
-    or two (profiles/r04/ab_streams.txt)."""
+    """The n streams consecutive steps alternate between: the library's own
+    compute streams (nt_dev_stream: the streams its host entry points pipeline
+    on, so the line measures the product's stream layout).
+    NT_BENCH_LIB_STREAMS=0 (A/B): `stream` and n - 1 more torch streams, as
+    rounds 1-4 did (profiles/r05/ab_streams.txt)."""
+    if os.environ.get("NT_BENCH_LIB_STREAMS", "1") != "0":
+        return [torch.cuda.ExternalStream(be.dev_stream(0, k), device=dev) for k in range(n)]
     if n == 1:
         return [stream]
-    if os.environ.get("NT_BENCH_LIB_STREAMS") == "1" and hasattr(be, "dev_stream"):
-        return [torch.cuda.ExternalStream(be.dev_stream(0, k), device=dev) for k in range(n)]
     return [stream] + [torch.cuda.Stream(dev) for _ in range(n - 1)]
 
 
@@ -183,12 +189,6 @@ def side_streams(torch, dev, n):
     pr = lo if os.environ.get("NT_BENCH_SIDE_PRIO", "high") == "normal" else hi
     return [torch.cuda.Stream(dev, priority=pr) for _ in range(n)]
 
-
-# wave issue priority of the config-3 digest launches (nt_dev_sha512_trunc32_bounded):
-# the certificate digests gate the next key-cache launch (highest), the header ids
-# on the side streams do not (lowest; their queue's priority already lifts them)
-CSHA_PRIO = int(os.environ.get("NT_BENCH_CSHA_PRIO", "3"))
-HSHA_PRIO = int(os.environ.get("NT_BENCH_HSHA_PRIO", "0"))
 
 _T0 = time.time()
 
@@ -284,7 +284,7 @@ def main():
     pk = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
     t0 = time.time()
-    be.dev_sign(0, sp, seeds.data_ptr(), msgs.data_ptr(), off.data_ptr(), ln.data_ptr(), n, pk.data_ptr(),
+    be.dev_sign(0, sp, seeds.data_ptr(), msgs.data_ptr(), nbytes(msgs), off.data_ptr(), ln.data_ptr(), n, pk.data_ptr(),
                 sig.data_ptr())
     torch.cuda.synchronize(dev)
     gen_s = time.time() - t0
@@ -335,11 +335,12 @@ def main():
         if timed:
             lev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
             lev[-1][0].record(st)
-        be.dev_verify(0, st.cuda_stream, ntcrypto.NT_MODE_STRICT, pk.data_ptr(), sig.data_ptr(), msgs.data_ptr(),
+        be.dev_verify(0, st.cuda_stream, ntcrypto.NT_MODE_STRICT, pk.data_ptr(), sig.data_ptr(), msgs.data_ptr(), nbytes(msgs),
                       off.data_ptr(), ln.data_ptr(), n, outs[i % nstreams].data_ptr())
         if timed:
             lev[-1][1].record(st)
 
+    barrier()  # the inputs were written on `stream`; the library's streams are ordered against no other
     for i in range(args.warmup):
         step(i)
     barrier()
@@ -555,7 +556,7 @@ def cfg2_two_streams(torch, be, dev, stream, ntcrypto, pk, sig, msgs, off, ln, n
 
     def step(i):
         be.dev_verify(0, streams[i % 2].cuda_stream, ntcrypto.NT_MODE_STRICT, pk.data_ptr(), sig.data_ptr(),
-                      msgs.data_ptr(), off.data_ptr(), ln.data_ptr(), n, outs[i % 2].data_ptr())
+                      msgs.data_ptr(), nbytes(msgs), off.data_ptr(), ln.data_ptr(), n, outs[i % 2].data_ptr())
 
     barrier()  # outs (zeroed on `stream`) are written on the pipeline streams
     for i in range(max(2, args.warmup)):
@@ -597,7 +598,7 @@ def bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_r
     out = torch.empty((m, 32), dtype=torch.uint8, device=dev)
 
     def step():
-        be.dev_sha512(0, sp, data.data_ptr(), off.data_ptr(), ln.data_ptr(), m, out.data_ptr())
+        be.dev_sha512(0, sp, data.data_ptr(), nbytes(data), off.data_ptr(), ln.data_ptr(), m, out.data_ptr())
 
     steps = max(1, min(args.steps, 5))
     for _ in range(max(1, args.warmup)):
@@ -646,7 +647,7 @@ def bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_r
                 continue
 
             def stepN():
-                be.dev_sha512(0, sp, data.data_ptr(), off.data_ptr(), ln.data_ptr(), mN, out.data_ptr())
+                be.dev_sha512(0, sp, data.data_ptr(), nbytes(data), off.data_ptr(), ln.data_ptr(), mN, out.data_ptr())
             stepN()
             barrier()
             e0 = torch.cuda.Event(enable_timing=True)
@@ -714,14 +715,14 @@ def bench_sha_real(args, torch, dev, be, sp, stream, world, rank, barrier, max_o
     torch.cuda.synchronize(dev)
 
     def timed(k, reps):
-        be.dev_sha512(0, sp, data.data_ptr(), off.data_ptr(), ln.data_ptr(), k, out.data_ptr())
+        be.dev_sha512(0, sp, data.data_ptr(), nbytes(data), off.data_ptr(), ln.data_ptr(), k, out.data_ptr())
         barrier()
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(stream)
         for _ in range(reps):
-            be.dev_sha512(0, sp, data.data_ptr(), off.data_ptr(), ln.data_ptr(), k, out.data_ptr())
+            be.dev_sha512(0, sp, data.data_ptr(), nbytes(data), off.data_ptr(), ln.data_ptr(), k, out.data_ptr())
         ev1.record(stream)
         barrier()
         return max_over_ranks(time.perf_counter() - t0) / reps, ev0.elapsed_time(ev1) / reps
@@ -839,20 +840,20 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
     h_off = torch.arange(G, dtype=torch.int64, device=dev) * hlen
     h_len = torch.full((G,), hlen, dtype=torch.int64, device=dev)
     ids = torch.empty((G, 32), dtype=torch.uint8, device=dev)
-    be.dev_sha512(0, sp, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, ids.data_ptr())
+    be.dev_sha512(0, sp, hdr_flat.data_ptr(), nbytes(hdr_flat), h_off.data_ptr(), h_len.data_ptr(), G, ids.data_ptr())
     # header signatures by the author over the id
     i_off = torch.arange(G, dtype=torch.int64, device=dev) * 32
     i_len = torch.full((G,), 32, dtype=torch.int64, device=dev)
     hsig = torch.empty((G, 64), dtype=torch.uint8, device=dev)
     tmp_pk = torch.empty((G, 32), dtype=torch.uint8, device=dev)
-    be.dev_sign(0, sp, seeds[author].contiguous().data_ptr(), ids.data_ptr(), i_off.data_ptr(), i_len.data_ptr(), G,
+    be.dev_sign(0, sp, seeds[author].contiguous().data_ptr(), ids.data_ptr(), nbytes(ids), i_off.data_ptr(), i_len.data_ptr(), G,
                 tmp_pk.data_ptr(), hsig.data_ptr())
     # certificate digest preimage: id || round_le || origin
     cpre = torch.cat([ids, hdr[:, 32:40], hdr[:, 0:32]], dim=1).contiguous()
     c_off = torch.arange(G, dtype=torch.int64, device=dev) * 72
     c_len = torch.full((G,), 72, dtype=torch.int64, device=dev)
     cdig = torch.empty((G, 32), dtype=torch.uint8, device=dev)
-    be.dev_sha512(0, sp, cpre.data_ptr(), c_off.data_ptr(), c_len.data_ptr(), G, cdig.data_ptr())
+    be.dev_sha512(0, sp, cpre.data_ptr(), nbytes(cpre), c_off.data_ptr(), c_len.data_ptr(), G, cdig.data_ptr())
     # 67 distinct voters per certificate, signatures over the certificate digest
     voters = torch.rand((G, nk), device=dev, generator=g).argsort(dim=1)[:, :quorum].contiguous()
     V = G * quorum
@@ -861,7 +862,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
     v_len = torch.full((V,), 32, dtype=torch.int64, device=dev)
     vsig = torch.empty((V, 64), dtype=torch.uint8, device=dev)
     vpk = torch.empty((V, 32), dtype=torch.uint8, device=dev)
-    be.dev_sign(0, sp, seeds[voters.reshape(-1)].contiguous().data_ptr(), cdig.data_ptr(), v_off.data_ptr(),
+    be.dev_sign(0, sp, seeds[voters.reshape(-1)].contiguous().data_ptr(), cdig.data_ptr(), nbytes(cdig), v_off.data_ptr(),
                 v_len.data_ptr(), V, vpk.data_ptr(), vsig.data_ptr())
     # 1 % of certificates carry one corrupted vote
     rng = np.random.default_rng(99 + rank)
@@ -932,14 +933,14 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
         # certificate digests first (the votes' message); the header-id digests
         # (3.3 KB serial chains, latency-bound) are only needed by the verdict, so
         # they go after the signature launch, where they overlap the other stream
-        be.dev_sha512(0, sq, cpre.data_ptr(), c_off.data_ptr(), c_len.data_ptr(), G, b["cd2"].data_ptr(), max_len=72, prio=CSHA_PRIO)
+        be.dev_sha512(0, sq, cpre.data_ptr(), nbytes(cpre), c_off.data_ptr(), c_len.data_ptr(), G, b["cd2"].data_ptr(), max_len=72)
         if not (cached and fused):
-            be.dev_sha512(0, sq, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, b["hd2"].data_ptr(),
+            be.dev_sha512(0, sq, hdr_flat.data_ptr(), nbytes(hdr_flat), h_off.data_ptr(), h_len.data_ptr(), G, b["hd2"].data_ptr(),
                           max_len=hlen)
         if cached and not fused:   # A/B reference: the header and vote launches separately
-            ks.dev_verify(0, sq, ntcrypto.NT_MODE_STRICT, hkey.data_ptr(), hsig.data_ptr(), ids.data_ptr(),
+            ks.dev_verify(0, sq, ntcrypto.NT_MODE_STRICT, hkey.data_ptr(), hsig.data_ptr(), ids.data_ptr(), nbytes(ids),
                           i_off.data_ptr(), i_len.data_ptr(), G, b["hbits"].data_ptr())
-            ks.dev_verify(0, sq, ntcrypto.NT_MODE_COFACTORLESS, vkey.data_ptr(), vsig.data_ptr(), b["cd2"].data_ptr(),
+            ks.dev_verify(0, sq, ntcrypto.NT_MODE_COFACTORLESS, vkey.data_ptr(), vsig.data_ptr(), b["cd2"].data_ptr(), nbytes(b["cd2"]),
                           v_off.data_ptr(), v_len.data_ptr(), V, b["vbits"].data_ptr())
             be.dev_group_and(0, sq, first.data_ptr(), cnt.data_ptr(), G, b["vbits"].data_ptr(), b["gbits"].data_ptr())
         elif cached:
@@ -948,24 +949,24 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                 kev[-1][0].record(st)
             if side and slots(cached) > 1:
                 # header ids beside the signature launch; the step's last kernel waits for them
-                be.dev_sha512(0, side[k].cuda_stream, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G,
-                              b["hd2"].data_ptr(), max_len=hlen, prio=HSHA_PRIO)
+                be.dev_sha512(0, side[k].cuda_stream, hdr_flat.data_ptr(), nbytes(hdr_flat), h_off.data_ptr(), h_len.data_ptr(), G,
+                              b["hd2"].data_ptr(), max_len=hlen)
                 hev = torch.cuda.Event()
                 hev.record(side[k])
-            ks.dev_verify(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(),
+            ks.dev_verify(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(), nbytes(b["msgbuf"]),
                           m_off.data_ptr(), m_len.data_ptr(), V + G, b["mbits"].data_ptr())
             if timed:
                 kev[-1][1].record(st)
             if side and slots(cached) > 1:
                 st.wait_event(hev)
             else:
-                be.dev_sha512(0, sq, hdr_flat.data_ptr(), h_off.data_ptr(), h_len.data_ptr(), G, b["hd2"].data_ptr(),
+                be.dev_sha512(0, sq, hdr_flat.data_ptr(), nbytes(hdr_flat), h_off.data_ptr(), h_len.data_ptr(), G, b["hd2"].data_ptr(),
                               max_len=hlen)
             be.dev_group_and(0, sq, first.data_ptr(), cnt.data_ptr(), G, b["mbits"].data_ptr(), b["gbits"].data_ptr())
         else:
-            be.dev_verify(0, sq, ntcrypto.NT_MODE_STRICT, tmp_pk.data_ptr(), hsig.data_ptr(), ids.data_ptr(),
+            be.dev_verify(0, sq, ntcrypto.NT_MODE_STRICT, tmp_pk.data_ptr(), hsig.data_ptr(), ids.data_ptr(), nbytes(ids),
                           i_off.data_ptr(), i_len.data_ptr(), G, b["hbits"].data_ptr())
-            be.dev_verify(0, sq, ntcrypto.NT_MODE_COFACTORLESS, vpk.data_ptr(), vsig.data_ptr(), b["cd2"].data_ptr(),
+            be.dev_verify(0, sq, ntcrypto.NT_MODE_COFACTORLESS, vpk.data_ptr(), vsig.data_ptr(), b["cd2"].data_ptr(), nbytes(b["cd2"]),
                           v_off.data_ptr(), v_len.data_ptr(), V, b["vbits"].data_ptr())
             be.dev_group_and(0, sq, first.data_ptr(), cnt.data_ptr(), G, b["vbits"].data_ptr(), b["gbits"].data_ptr())
 
@@ -1034,6 +1035,40 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
             rf["launch_ms_one_stream"] = round(own, 3)
             rf["frac_one_stream_launch"] = round(ach / MAD_PEAK_TS, 4)
         progress("cfg3 %s: %.2f M certificates/s" % (key, out[key]["certs_per_s"] / 1e6))
+    if os.environ.get("NT_BENCH_STREAM_AB") == "1" and fused and world == 1:
+        # diagnosis: the same one-stream key-cache steps on each
+        # candidate stream, interleaved twice, in one process
+        saved = list(streams)
+        lib = [torch.cuda.ExternalStream(be.dev_stream(0, k), device=dev) for k in range(2)]
+        cands = [("lib0", lib[0]), ("lib1", lib[1]), ("torch_cur", stream), ("torch_new", torch.cuda.Stream(dev))]
+        ab = []
+        mode_streams[True] = 1
+        for name, st in cands * 2:
+            streams[0] = st
+            barrier()
+            for i in range(2):
+                step(True, i)
+            barrier()
+            kev.clear()
+            t0 = time.perf_counter()
+            for i in range(20):
+                step(True, i, timed=True)
+            barrier()
+            wall = time.perf_counter() - t0
+            ab.append({"stream": name, "certs_per_s": round(G * 20 / wall, 1),
+                       "launch_ms": round(float(np.mean([a.elapsed_time(b) for a, b in kev])), 3)})
+        streams[:] = saved
+        mode_streams[True] = nst
+        out["stream_ab"] = ab
+        progress("cfg3 stream A/B")
+    # -------- the same votes through the host entry point (what the crate's FFI binds)
+    # nt_ed25519_verify_batch_groups_keyset: Certificate::verify's verify_batch of the
+    # 67 votes per certificate (crypto/src/lib.rs:206-219), keys as committee indices,
+    # inputs in nt_host_alloc (pinned) memory: PCIe-inclusive, never `value`
+    if os.environ.get("NT_BENCH_HOST_CERTS", "1") != "0":
+        out["host_api"] = bench_cert_host_api(be, ks, vkey, vsig, cdig, G, quorum, expect, barrier,
+                                              max_over_ranks, world, G_total)
+        progress("cfg3 host entry point: %.2f M certificates/s" % (out["host_api"]["certs_per_s"] / 1e6))
     if world == 1 and fused and os.environ.get("NT_BENCH_SHARDS", "1") != "0":
         out["shard_of"] = bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream, barrier, G,
                                             quorum,
@@ -1044,6 +1079,22 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                                                  cnt=cnt),
                                             expect, out["keyset"]["certs_per_s"])
         progress("cfg3 shards")
+        if os.environ.get("NT_BENCH_STREAM_AB") == "1":
+            # the same shard steps on two torch streams (rounds 1-4's layout), same process
+            tst = [stream, torch.cuda.Stream(dev)]
+            out["shard_of_torch_streams"] = bench_cert_shards(
+                args, torch, dev, ks, be, ntcrypto, tst, side, stream, barrier, G, quorum,
+                dict(hdr_flat=hdr_flat, h_off=h_off, h_len=h_len, hlen=hlen, cpre=cpre, c_off=c_off, c_len=c_len,
+                     ids=ids, vkey=vkey, hkey=hkey, vsig=vsig, hsig=hsig, v_off=v_off, v_len=v_len, i_off=i_off,
+                     i_len=i_len, first=first, cnt=cnt),
+                expect, out["keyset"]["certs_per_s"])
+            out["shard_of_lib_again"] = bench_cert_shards(
+                args, torch, dev, ks, be, ntcrypto, streams, side, stream, barrier, G, quorum,
+                dict(hdr_flat=hdr_flat, h_off=h_off, h_len=h_len, hlen=hlen, cpre=cpre, c_off=c_off, c_len=c_len,
+                     ids=ids, vkey=vkey, hkey=hkey, vsig=vsig, hsig=hsig, v_off=v_off, v_len=v_len, i_off=i_off,
+                     i_len=i_len, first=first, cnt=cnt),
+                expect, out["keyset"]["certs_per_s"])
+            progress("cfg3 shards A/B")
     ks.close()
     if world == 1 and not getattr(args, "no_cpu", False):
         out["cpu_baseline"] = cert_cpu_baseline(args, hdr, hlen, ids, tmp_pk, hsig, cpre, vpk, vsig, quorum, expect)
@@ -1065,6 +1116,38 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                                       "(67 votes cofactorless + the header signature strict), SHA-512 of the header "
                                       "ids (only the verdict needs them), 1 group AND"},
             **out}
+
+
+def bench_cert_host_api(be, ks, vkey, vsig, cdig, G, quorum, expect, barrier, max_over_ranks, world, G_total,
+                        reps=3):
+    """Config 3's votes through nt_ed25519_verify_batch_groups_keyset from pinned
+    host buffers: G certificates x `quorum` votes, keys as
+    committee indices, one 32-byte certificate digest per group.  The library
+    stages nothing (the inputs are nt_host_alloc memory and densely packed):
+    chunk c+1's copies run under chunk c's key-cache launch on the library's two
+    compute streams.  Verdicts checked against the expected group results."""
+    key_p = be.pinned((G * quorum,), np.uint32)
+    sig_p = be.pinned((G * quorum, 64))
+    key_p[...] = vkey.cpu().numpy().view(np.uint32)
+    sig_p[...] = vsig.cpu().numpy()
+    msg32 = cdig.cpu().numpy()
+    first = np.arange(G, dtype=np.uint64) * quorum
+    cnt = np.full(G, quorum, np.uint32)
+    got = ks.verify_batch_groups(key_p, sig_p, first, cnt, msg32)   # warm-up (stash, staging)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        got = ks.verify_batch_groups(key_p, sig_p, first, cnt, msg32)
+    barrier()
+    wall = max_over_ranks((time.perf_counter() - t0) / reps)
+    mism = int(max_over_ranks(int((got != expect).sum())))
+    del key_p, sig_p
+    return {"certs_per_s": round(G_total / wall, 1), "sig_verifies_per_s": round(G_total * quorum / wall, 1),
+            "ms_per_call": round(wall * 1e3, 3), "mismatches_vs_expected": mism,
+            "bytes_per_call": int(G * quorum * 68 + G * 44),
+            "note": "nt_ed25519_verify_batch_groups_keyset on %d certificates x %d votes per rank from nt_host_alloc "
+                    "buffers (4-B key index + 64-B signature per vote over PCIe; no staging copy), the library's "
+                    "chunk pipeline on its own streams; PCIe-inclusive, never `value`" % (G, quorum)}
 
 
 def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream, barrier, G,
@@ -1111,24 +1194,24 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream,
             st = streams[i % nst]
             sq = st.cuda_stream
             b = bufs[i % nst]
-            be.dev_sha512(0, sq, t["cpre"].data_ptr(), t["c_off"].data_ptr(), t["c_len"].data_ptr(), Gs,
-                          b["msgbuf"].data_ptr(), max_len=72, prio=CSHA_PRIO)
+            be.dev_sha512(0, sq, t["cpre"].data_ptr(), nbytes(t["cpre"]), t["c_off"].data_ptr(), t["c_len"].data_ptr(), Gs,
+                          b["msgbuf"].data_ptr(), max_len=72)
             if timed:
                 kev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
                 kev[-1][0].record(st)
             if side:
-                be.dev_sha512(0, side[i % nst].cuda_stream, t["hdr_flat"].data_ptr(), t["h_off"].data_ptr(),
-                              t["h_len"].data_ptr(), Gs, b["hd2"].data_ptr(), max_len=t["hlen"], prio=HSHA_PRIO)
+                be.dev_sha512(0, side[i % nst].cuda_stream, t["hdr_flat"].data_ptr(), nbytes(t["hdr_flat"]), t["h_off"].data_ptr(),
+                              t["h_len"].data_ptr(), Gs, b["hd2"].data_ptr(), max_len=t["hlen"])
                 hev = torch.cuda.Event()
                 hev.record(side[i % nst])
-            ks.dev_verify(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(),
+            ks.dev_verify(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(), nbytes(b["msgbuf"]),
                           m_off.data_ptr(), m_len.data_ptr(), Vs + Gs, b["mbits"].data_ptr())
             if timed:
                 kev[-1][1].record(st)
             if side:
                 st.wait_event(hev)
             else:
-                be.dev_sha512(0, sq, t["hdr_flat"].data_ptr(), t["h_off"].data_ptr(), t["h_len"].data_ptr(), Gs,
+                be.dev_sha512(0, sq, t["hdr_flat"].data_ptr(), nbytes(t["hdr_flat"]), t["h_off"].data_ptr(), t["h_len"].data_ptr(), Gs,
                               b["hd2"].data_ptr(), max_len=t["hlen"])
             be.dev_group_and(0, sq, t["first"].data_ptr(), t["cnt"].data_ptr(), Gs, b["mbits"].data_ptr(),
                              b["gbits"].data_ptr())

@@ -37,8 +37,9 @@
  *     over the context's devices (certificates are never split); no
  *     collective, results gathered on the host.
  *   - nt_dev_* entry points take DEVICE pointers on device `dev` of the
- *     context and a hipStream_t (NULL = the library's stream), and only
- *     enqueue work.  Word-typed buffers (pk, sig, seed, out) must be 16-byte
+ *     context and a hipStream_t (NULL = HIP's NULL stream), and only
+ *     enqueue work; message buffers come with their byte size and the
+ *     kernels never read outside it.  Word-typed buffers (pk, sig, seed, out) must be 16-byte
  *     aligned; message data may have any alignment.
  */
 #ifndef NTCRYPTO_H
@@ -257,52 +258,59 @@ void *nt_host_alloc(uint64_t bytes);
 void nt_host_free(void *p);
 
 /* ---- device-resident entry points (enqueue only) ----------------------
- * Batches enqueued back to back on two streams overlap only if the two streams
- * sit on different hardware queues: HIP multiplexes a process's streams over
- * GPU_MAX_HW_QUEUES (4) queues and may hand two streams the same one, whose
- * kernels then run strictly in order.  nt_dev_stream returns device entry
- * `dev`'s two compute streams (which = 0 / 1), created on queues of their own
- * (a CU-masked stream never shares its queue; the mask enables every CU): a
- * caller pipelining device-API batches may alternate between them or between
- * two streams of its own (with the library's streams on queues of their own,
- * the caller's two get separate shared queues; measured, the same launches ran
- * 3-5 % faster on the caller's torch streams: DESIGN.md §8).  They
- * are ordered against no other stream: inputs produced elsewhere (a framework's
- * stream, a copy) must be complete -- an event the stream waits on, or a
- * synchronize -- before the first call that reads them.  The kernels trust
- * d_off / d_len; an offset read before it was written is a wild access. */
+ * `stream` is the caller's hipStream_t; NULL is HIP's NULL stream, as for any
+ * HIP call (round 4 read NULL as "the library's stream").  The calls order
+ * their launches after earlier work on `stream` only: inputs produced on
+ * another stream must be complete (an event `stream` waits on, or a
+ * synchronize) before the call.
+ *
+ * Message buffers come with their byte size (msg_bytes / data_bytes): item i
+ * reads d_msg[d_off[i] .. d_off[i] + d_len[i]) only when that slice lies inside
+ * [0, msg_bytes).  An item whose slice does not is never read -- a verification
+ * rejects it, signing writes an all-zero signature, SHA-512 writes a zero
+ * digest and adds 1 to *d_bad (a device counter the caller zeroes; NULL = not
+ * counted).  So an offset read before its producer wrote it (round 4's fault
+ * r04e: a wild offset from a cross-stream race) cannot fault the card.
+ *
+ * nt_dev_stream returns device entry `dev`'s two compute streams (which = 0 /
+ * 1), the streams the host entry points pipeline on: non-blocking, ordered
+ * against no other stream (NT_STREAMS=mask: each on a hardware queue of its
+ * own, but then BLOCKING, i.e. ordered against the NULL stream).  Batches
+ * enqueued back to back overlap only if their streams sit on different
+ * hardware queues (HIP multiplexes a process's streams over GPU_MAX_HW_QUEUES
+ * queues per priority); a caller pipelining device-API batches may alternate
+ * between these two or two of its own. */
 int nt_dev_stream(nt_ctx *ctx, int dev, int which, void **out);
-int nt_dev_sha512_trunc32(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_data,
-                          const uint64_t *d_off, const uint64_t *d_len, uint64_t n,
+int nt_dev_sha512_trunc32(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_data, uint64_t data_bytes,
+                          const uint64_t *d_off, const uint64_t *d_len, uint64_t n, uint32_t *d_bad,
                           uint8_t *d_out32);
 /* The same digests when the caller knows an upper bound of the lengths
  * (headers, votes, certificate digests): max_len only selects the kernel --
  * below 16 KB the one-lane kernel, which holds no LDS, so it never waits
  * behind a key-cache launch of another stream.  Any length is
- * still hashed correctly whatever max_len says.  prio: the launch's wave issue
- * priority, 0..3 (-1 = the default, 2): a digest launch that a pipeline waits
- * on beside long launches goes first at 3; one off the critical path at 0. */
+ * still hashed correctly whatever max_len says. */
 int nt_dev_sha512_trunc32_bounded(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_data,
-                                  const uint64_t *d_off, const uint64_t *d_len, uint64_t n,
-                                  uint64_t max_len, int prio, uint8_t *d_out32);
+                                  uint64_t data_bytes, const uint64_t *d_off, const uint64_t *d_len, uint64_t n,
+                                  uint64_t max_len, uint32_t *d_bad, uint8_t *d_out32);
 /* d_out_words: ceil(n/64) little-endian 64-bit bitmap words.  Successive calls
  * alternate between the device entry's two [k]A workspaces (each ordered by
  * its own event), so batches enqueued back to back on two different streams
  * overlap: the next batch's waves fill the SIMDs the previous batch's last
  * round leaves idle.  Calls on one stream run in stream order. */
 int nt_dev_ed25519_verify(nt_ctx *ctx, int dev, void *stream, int mode, const uint8_t *d_pk32,
-                          const uint8_t *d_sig64, const uint8_t *d_msg, const uint64_t *d_off,
-                          const uint64_t *d_len, uint64_t n, uint64_t *d_out_words);
+                          const uint8_t *d_sig64, const uint8_t *d_msg, uint64_t msg_bytes,
+                          const uint64_t *d_off, const uint64_t *d_len, uint64_t n, uint64_t *d_out_words);
 int nt_dev_group_and(nt_ctx *ctx, int dev, void *stream, const uint64_t *d_first,
                      const uint32_t *d_cnt, uint64_t G, const uint64_t *d_sig_words,
                      uint64_t *d_group_words);
 int nt_dev_ed25519_verify_keyset(nt_ctx *ctx, const nt_keyset *ks, int dev, void *stream, int mode,
-                                 const uint32_t *d_key_idx, const uint8_t *d_sig64,
-                                 const uint8_t *d_msg, const uint64_t *d_off, const uint64_t *d_len,
-                                 uint64_t n, uint64_t *d_out_words);
-int nt_dev_ed25519_sign(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_seed32,
-                        const uint8_t *d_msg, const uint64_t *d_off, const uint64_t *d_len,
-                        uint64_t n, uint8_t *d_pk32, uint8_t *d_sig64);
+                                 const uint32_t *d_key_idx, const uint8_t *d_sig64, const uint8_t *d_msg,
+                                 uint64_t msg_bytes, const uint64_t *d_off, const uint64_t *d_len, uint64_t n,
+                                 uint64_t *d_out_words);
+/* d_sig64 may be NULL (keygen only; d_msg, d_off, d_len ignored). */
+int nt_dev_ed25519_sign(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_seed32, const uint8_t *d_msg,
+                        uint64_t msg_bytes, const uint64_t *d_off, const uint64_t *d_len, uint64_t n,
+                        uint8_t *d_pk32, uint8_t *d_sig64);
 
 #ifdef __cplusplus
 }

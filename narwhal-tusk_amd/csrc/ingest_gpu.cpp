@@ -286,13 +286,15 @@ int ingest_back(Device& dv, IngestState& S, Side& sd, int parity, Chunk& ch, con
   b.smlen = b.smoff + nsig;
   b.sig_words = sd.words.as<uint64_t>();
   NT_TRY(nt::launch_cert_scatter(pd.c, b, s));
-  NT_TRY(nt::launch_sha512_trunc32(b.mbase, b.soff, b.slen, 2 * m, b.mbase + 32 * m, s, std::max<uint64_t>(ch.lmax, 72)));
+  const uint64_t mbytes = 168 * m + 16 + P;  // the preimages and digests k_cert_scatter wrote
+  NT_TRY(nt::launch_sha512_trunc32(b.mbase, mbytes, b.soff, b.slen, 2 * m, b.mbase + 32 * m, s,
+                                   std::max<uint64_t>(ch.lmax, 72)));
   NT_CHK0(dv.ensure_stash(parity, nsig));
   void* st = parity ? dv.stash2.p : dv.d[B_STASH].p;
   void* so = parity ? dv.sort2.p : dv.d[B_SORT].p;
   const auto& kd = cm.kt->dev[dv.group];
   NT_CHK0(dv.keyset_launch(s, st, [&] {
-    return nt::launch_verify_keyset(NT_MODE_MIXED, cm.kt->bits, b.keys, (const uint8_t*)b.sigs, b.mbase, b.smoff,
+    return nt::launch_verify_keyset(NT_MODE_MIXED, cm.kt->bits, b.keys, (const uint8_t*)b.sigs, b.mbase, mbytes, b.smoff,
                                     b.smlen, nsig, kd.d_meta, kd.d_enc, kd.d_comb, cm.kt->nkeys, dv.d_combB, dv.bbits,
                                     st, so, sd.words.as<uint64_t>(), dv.cus, s);
   }));

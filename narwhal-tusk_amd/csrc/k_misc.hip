@@ -33,37 +33,58 @@ namespace nt {
 // --------------------------------------------------------------------------
 // SHA-512 digests
 // --------------------------------------------------------------------------
-NT_D NT_INLINE void sha512_trunc32_one(const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
-                                       const uint64_t* __restrict__ len, uint64_t n, uint32_t* __restrict__ out) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  uint64_t st[8];
-  sha512_prefixed<0>(st, nullptr, data + off[i], len[i]);
+// digest of an out-of-bounds item (msg_slice): 32 zero bytes, counted in *bad
+// (when the caller passed a counter) -- the message is never read
+NT_D NT_INLINE void sha512_put(uint32_t* __restrict__ out, uint64_t i, const uint64_t st[8], uint32_t ok,
+                               uint32_t* __restrict__ bad) {
   uint32_t w[8];
   sha512_out_words(w, st, 8);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) w[q] = ok ? w[q] : 0u;
   uint4* o = (uint4*)(out + 8 * i);
   o[0] = make_uint4(w[0], w[1], w[2], w[3]);
   o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  if (!ok && bad) atomicAdd(bad, 1u);
 }
-__global__ __launch_bounds__(kBlock) void k_sha512_trunc32(const uint8_t* __restrict__ data,
+NT_D NT_INLINE void sha512_trunc32_one(const uint8_t* __restrict__ data, uint64_t data_bytes,
+                                       const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t n,
+                                       uint32_t* __restrict__ out, uint32_t* __restrict__ bad) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const MsgSlice ms = msg_slice(off[i], len[i], data_bytes);
+  uint64_t st[8];
+  sha512_prefixed<0>(st, nullptr, data + ms.off, ms.len);
+  sha512_put(out, i, st, ms.ok, bad);
+}
+__global__ __launch_bounds__(kBlock) void k_sha512_trunc32(const uint8_t* __restrict__ data, uint64_t data_bytes,
                                                           const uint64_t* __restrict__ off,
                                                           const uint64_t* __restrict__ len,
-                                                          uint64_t n, uint32_t* __restrict__ out, int prio) {
-  wave_priority(prio);
-  sha512_trunc32_one(data, off, len, n, out);
+                                                          uint64_t n, uint32_t* __restrict__ out,
+                                                          uint32_t* __restrict__ bad) {
+  aux_priority();
+  sha512_trunc32_one(data, data_bytes, off, len, n, out, bad);
 }
-// The same for short messages (<= kLeanMaxLen bytes: certificate / vote
-// digests) in at most 64 VGPRs (8 waves per SIMD; the compression spills a
-// little): beside two co-resident key-cache launches (4 x 112 VGPRs per SIMD)
-// only 64 are free, and a launch that needs more waits for one of them to end
-// (tools/microbench/co_dispatch.hip).
+// The same for short messages (<= kLeanMaxLen bytes) in at most 64 VGPRs (8
+// waves per SIMD; the compression spills ~476 B per lane): beside two
+// co-resident key-cache launches (4 x 112 VGPRs per SIMD) only 64 are free
+// (tools/microbench/co_dispatch.hip).  Off by default: the
+// 8-GPU shard measured 11.31 M certificates/s with it against 11.43 without
+// (round 4, profiles/r04/ab_r04u/); -DNT_SHA_LEAN_MAX=256 builds it in (A/B).
+#ifndef NT_SHA_LEAN_MAX
+#define NT_SHA_LEAN_MAX 0
+#endif
+[[maybe_unused]] constexpr uint64_t kLeanMaxLen = NT_SHA_LEAN_MAX;
+#if NT_SHA_LEAN_MAX > 0
 __global__ __launch_bounds__(kBlock, 8) void k_sha512_trunc32_lean(const uint8_t* __restrict__ data,
+                                                                   uint64_t data_bytes,
                                                                    const uint64_t* __restrict__ off,
                                                                    const uint64_t* __restrict__ len,
-                                                                   uint64_t n, uint32_t* __restrict__ out, int prio) {
-  wave_priority(prio);
-  sha512_trunc32_one(data, off, len, n, out);
+                                                                   uint64_t n, uint32_t* __restrict__ out,
+                                                                   uint32_t* __restrict__ bad) {
+  aux_priority();
+  sha512_trunc32_one(data, data_bytes, off, len, n, out, bad);
 }
+#endif
 
 // Few long messages (n <= kPipeMaxMsgs, e.g. config 4: 16,384 x 500 kB): one
 // lane per message is latency-bound (the per-block instruction stream of a
@@ -80,10 +101,6 @@ constexpr int kPipeMaxMsgs = 32768;  // 80 KB LDS per workgroup: 2 per CU
 // queued behind them then waits for that launch's tail (rocprofv3 trace,
 // DESIGN.md §10).
 constexpr uint64_t kPipeMinLen = 16384;
-#ifndef NT_SHA_LEAN_MAX
-#define NT_SHA_LEAN_MAX 256
-#endif
-constexpr uint64_t kLeanMaxLen = NT_SHA_LEAN_MAX;  // 0 disables the lean kernel (A/B)
 struct KwLdsSink {
   uint4* slot;  // [40][64]
   uint32_t lane;
@@ -109,19 +126,20 @@ struct KwPrefetchSource {
   }
 };
 
-__global__ __launch_bounds__(128) void k_sha512_pipe(const uint8_t* __restrict__ data,
+__global__ __launch_bounds__(128) void k_sha512_pipe(const uint8_t* __restrict__ data, uint64_t data_bytes,
                                                      const uint64_t* __restrict__ off,
                                                      const uint64_t* __restrict__ len, uint64_t n,
-                                                     uint32_t* __restrict__ out, int prio) {
-  wave_priority(prio);
+                                                     uint32_t* __restrict__ out, uint32_t* __restrict__ bad) {
+  aux_priority();
   __shared__ uint4 ring[2][40 * 64];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = threadIdx.x >> 6;
   const uint64_t gi = (uint64_t)blockIdx.x * 64 + lane;
   const bool act = gi < n;
   const uint64_t i = act ? gi : n - 1;
-  const uint8_t* msg = data + off[i];
-  const uint64_t ln = len[i];
+  const MsgSlice ms = msg_slice(off[i], len[i], data_bytes);
+  const uint8_t* msg = data + ms.off;
+  const uint64_t ln = ms.len;
   const uint64_t nblocks = (ln + 17 + 127) / 128;
   const uint64_t nfull = ln / 128;
   // trip count shared by both waves (same 64 messages): max over the lanes
@@ -176,13 +194,7 @@ __global__ __launch_bounds__(128) void k_sha512_pipe(const uint8_t* __restrict__
       }
       __syncthreads();
     }
-    if (act) {
-      uint32_t w[8];
-      sha512_out_words(w, st, 8);
-      uint4* o = (uint4*)(out + 8 * gi);
-      o[0] = make_uint4(w[0], w[1], w[2], w[3]);
-      o[1] = make_uint4(w[4], w[5], w[6], w[7]);
-    }
+    if (act) sha512_put(out, gi, st, ms.ok, bad);
   }
 }
 
@@ -280,7 +292,7 @@ __global__ __launch_bounds__(kBlock) void k_group_and(const uint64_t* __restrict
 // --------------------------------------------------------------------------
 template <int WB>
 __global__ __launch_bounds__(kBlock) void k_ed25519_sign(const uint32_t* __restrict__ seed,
-                                                        const uint8_t* __restrict__ msg,
+                                                        const uint8_t* __restrict__ msg, uint64_t msg_bytes,
                                                         const uint64_t* __restrict__ off,
                                                         const uint64_t* __restrict__ len, uint64_t n,
                                                         const uint32_t* __restrict__ combB,
@@ -294,9 +306,14 @@ __global__ __launch_bounds__(kBlock) void k_ed25519_sign(const uint32_t* __restr
     uint32_t sw[8];
     ld8(sw, seed + 8 * i);
     uint32_t Aw[8], Rw[8], s[8];
-    const uint8_t* m = msg ? msg + off[i] : nullptr;
-    const uint64_t ml = msg ? len[i] : 0;
-    sign_one(Aw, Rw, s, sw, m, ml, wb);
+    // an out-of-bounds message (msg_slice): nothing read, an all-zero signature
+    const MsgSlice ms = msg ? msg_slice(off[i], len[i], msg_bytes) : MsgSlice{0, 0, 1};
+    sign_one(Aw, Rw, s, sw, msg ? msg + ms.off : nullptr, ms.len, wb);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      Rw[q] = ms.ok ? Rw[q] : 0u;
+      s[q] = ms.ok ? s[q] : 0u;
+    }
     if (active) {
       uint4* po = (uint4*)(out_pk + 8 * i);
       po[0] = make_uint4(Aw[0], Aw[1], Aw[2], Aw[3]);
@@ -315,21 +332,25 @@ __global__ __launch_bounds__(kBlock) void k_ed25519_sign(const uint32_t* __restr
 // --------------------------------------------------------------------------
 // Launchers (host)
 // --------------------------------------------------------------------------
-hipError_t launch_sha512_trunc32(const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
-                                 uint64_t n, uint8_t* d_out32, hipStream_t s, uint64_t max_len, int prio) {
+hipError_t launch_sha512_trunc32(const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_off,
+                                 const uint64_t* d_len, uint64_t n, uint8_t* d_out32, hipStream_t s, uint64_t max_len,
+                                 uint32_t* d_bad) {
   if (n == 0) return hipSuccess;
   if (n <= (uint64_t)kPipeMaxMsgs && max_len >= kPipeMinLen && !std::getenv("NT_SHA_NO_PIPE")) {
-    hipLaunchKernelGGL(k_sha512_pipe, dim3((uint32_t)((n + 63) / 64)), dim3(128), 0, s, d_data, d_off, d_len, n,
-                       (uint32_t*)d_out32, prio);
+    hipLaunchKernelGGL(k_sha512_pipe, dim3((uint32_t)((n + 63) / 64)), dim3(128), 0, s, d_data, data_bytes, d_off,
+                       d_len, n, (uint32_t*)d_out32, d_bad);
     return hipGetLastError();
   }
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
-  if (max_len <= kLeanMaxLen)
-    hipLaunchKernelGGL(k_sha512_trunc32_lean, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_data, d_off, d_len, n,
-                       (uint32_t*)d_out32, prio);
-  else
-    hipLaunchKernelGGL(k_sha512_trunc32, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_data, d_off,
-                       d_len, n, (uint32_t*)d_out32, prio);
+#if NT_SHA_LEAN_MAX > 0
+  if (max_len <= kLeanMaxLen) {
+    hipLaunchKernelGGL(k_sha512_trunc32_lean, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_data, data_bytes, d_off,
+                       d_len, n, (uint32_t*)d_out32, d_bad);
+    return hipGetLastError();
+  }
+#endif
+  hipLaunchKernelGGL(k_sha512_trunc32, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_data, data_bytes, d_off, d_len, n,
+                     (uint32_t*)d_out32, d_bad);
   return hipGetLastError();
 }
 
@@ -345,13 +366,13 @@ int verify_occupancy() { return verify_occ(); }
 int keyset_occupancy() { return keyset_occ(); }
 
 hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
-                         const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
+                         uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
                          const uint32_t* d_combB, int bbits, void* d_ws, uint32_t ws_slots, uint64_t* d_out_words,
                          hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (!d_combB || !d_ws) return hipErrorInvalidValue;
   const uint64_t blocks = verify_grid(n, ws_slots);
-#define NT_V_ARGS blocks, d_pk, d_sig, d_msg, d_off, d_len, n, d_combB, d_ws, d_out_words, s
+#define NT_V_ARGS blocks, d_pk, d_sig, d_msg, msg_bytes, d_off, d_len, n, d_combB, d_ws, d_out_words, s
   if (bbits == kBCombBits)
     return mode == kStrict ? launch_verify_m<kStrict, kBCombBits>(NT_V_ARGS)
                            : launch_verify_m<kCofactorless, kBCombBits>(NT_V_ARGS);
@@ -380,7 +401,7 @@ hipError_t launch_group_msgs(const uint64_t* d_first, const uint32_t* d_cnt, uin
   return hipGetLastError();
 }
 
-hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, const uint64_t* d_off,
+hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, uint64_t msg_bytes, const uint64_t* d_off,
                        const uint64_t* d_len, uint64_t n, const uint32_t* d_combB, int bbits, uint8_t* d_pk,
                        uint8_t* d_sig, uint32_t max_blocks, hipStream_t s) {
   if (n == 0) return hipSuccess;
@@ -389,7 +410,7 @@ hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, const uint64
   if (blocks > max_blocks) blocks = max_blocks;
 #define NT_SIGN_LAUNCH(WB)                                                                              \
   hipLaunchKernelGGL(k_ed25519_sign<WB>, dim3((uint32_t)blocks), dim3(kBlock), 0, s,                   \
-                     (const uint32_t*)d_seed, d_msg, d_off, d_len, n, d_combB, (uint32_t*)d_pk, (uint32_t*)d_sig)
+                     (const uint32_t*)d_seed, d_msg, msg_bytes, d_off, d_len, n, d_combB, (uint32_t*)d_pk, (uint32_t*)d_sig)
   if (bbits == kBCombBits) NT_SIGN_LAUNCH(kBCombBits);
   else if (bbits == kBCombFallback) NT_SIGN_LAUNCH(kBCombFallback);
   else return hipErrorInvalidValue;
@@ -583,7 +604,7 @@ KsPlan keyset_plan(uint64_t n, uint32_t cus) {
 }
 
 hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
-                                const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
+                                uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                                 const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
                                 const uint32_t* d_combB, int bbits, void* d_stash, void* d_sort, uint64_t* d_out_words,
                                 uint32_t cus, hipStream_t s) {
@@ -617,7 +638,7 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
       perm = p;
     }
 #define NT_KS_ARGS                                                                                           \
-  pl, d_key_idx + lo, d_sig + 64 * lo, d_msg, d_off + lo, d_len + lo, m, d_meta, d_enc, d_combA, nkeys,     \
+  pl, d_key_idx + lo, d_sig + 64 * lo, d_msg, msg_bytes, d_off + lo, d_len + lo, m, d_meta, d_enc, d_combA, nkeys,     \
       d_combB, d_stash, d_out_words + lo / 64, perm, bytes, ctr, s
 #define NT_KS_MODES(WA, WB)                                                  \
   (mode == kStrict  ? launch_keyset_m<kStrict, WA, WB>(NT_KS_ARGS)            \

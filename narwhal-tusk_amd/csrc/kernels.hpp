@@ -9,14 +9,17 @@
 
 namespace nt {
 
+// Every launcher that reads caller messages takes the byte size of the message
+// buffer (msg_bytes / data_bytes): items whose slice lies outside it are never
+// read (nt_common.hpp msg_slice) -- rejected by verification and signing, a
+// zero digest counted in *d_bad (nullable) by SHA-512.
 // max_len: an upper bound of the messages' lengths when the caller knows one
-// (it selects the kernel; any length is still hashed correctly); prio: wave
-// issue priority 0..3 of the launch, < 0 = the build default (NT_AUX_PRIO)
-hipError_t launch_sha512_trunc32(const uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
-                                 uint64_t n, uint8_t* d_out32, hipStream_t s, uint64_t max_len = ~0ull,
-                                 int prio = -1);
+// (it selects the kernel; any length is still hashed correctly)
+hipError_t launch_sha512_trunc32(const uint8_t* d_data, uint64_t data_bytes, const uint64_t* d_off,
+                                 const uint64_t* d_len, uint64_t n, uint8_t* d_out32, hipStream_t s,
+                                 uint64_t max_len = ~0ull, uint32_t* d_bad = nullptr);
 hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
-                         const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
+                         uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
                          const uint32_t* d_combB, int bbits, void* d_ws, uint32_t ws_slots, uint64_t* d_out_words,
                          hipStream_t s);
 hipError_t launch_group_and(const uint64_t* d_first, const uint32_t* d_cnt, uint64_t G,
@@ -24,7 +27,7 @@ hipError_t launch_group_and(const uint64_t* d_first, const uint32_t* d_cnt, uint
 // off[first[g] + q] = 32 g, len = 32 for q < cnt[g] (groups' 32-byte messages)
 hipError_t launch_group_msgs(const uint64_t* d_first, const uint32_t* d_cnt, uint64_t G, uint64_t* d_off,
                              uint64_t* d_len, hipStream_t s);
-hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, const uint64_t* d_off,
+hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, uint64_t msg_bytes, const uint64_t* d_off,
                        const uint64_t* d_len, uint64_t n, const uint32_t* d_combB, int bbits, uint8_t* d_pk,
                        uint8_t* d_sig, uint32_t max_blocks, hipStream_t s);
 // wide combs with `bits`-bit digits (a key-comb width, or kBCombBits for B; kBCombFallback = kKeyCombWide).
@@ -33,7 +36,7 @@ hipError_t launch_wcomb_build(int bits, const uint32_t* d_enc, uint32_t nkeys, i
                               uint32_t* d_meta, uint32_t* d_bases, uint32_t* d_tmp, uint32_t batch,
                               hipStream_t s);
 hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
-                                const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
+                                uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                                 const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
                                 const uint32_t* d_combB, int bbits, void* d_stash, void* d_sort, uint64_t* d_out_words,
                                 uint32_t cus, hipStream_t s);

@@ -28,14 +28,6 @@ NT_D NT_INLINE void aux_priority() {
   __builtin_amdgcn_s_setprio(NT_AUX_PRIO);
 #endif
 }
-// a launch-time priority (the digest launches: nt_dev_sha512_trunc32_bounded);
-// < 0 = the build's default above
-NT_D NT_INLINE void wave_priority(int p) {
-  if (p < 0) aux_priority();
-  else if (p == 1) __builtin_amdgcn_s_setprio(1);
-  else if (p == 2) __builtin_amdgcn_s_setprio(2);
-  else if (p >= 3) __builtin_amdgcn_s_setprio(3);
-}
 #ifndef NT_VERIFY_PER_LANE
 #define NT_VERIFY_PER_LANE 2
 #endif
@@ -231,11 +223,11 @@ struct KsStash {
 // committee keys' comb width.
 template <int MODE, int WB>
 hipError_t launch_verify_m(uint64_t blocks, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
-                           const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_combB,
-                           void* d_ws, uint64_t* d_out_words, hipStream_t s);
+                           uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
+                           const uint32_t* d_combB, void* d_ws, uint64_t* d_out_words, hipStream_t s);
 template <int MODE, int WA, int WB>
 hipError_t launch_keyset_m(const KsPlan& plan, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
-                           const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
+                           uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                            const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
                            const uint32_t* d_combB, void* d_stash, uint64_t* d_out_words, const uint32_t* d_perm,
                            uint8_t* d_out_bytes, uint32_t* d_chunk_ctr, hipStream_t s);

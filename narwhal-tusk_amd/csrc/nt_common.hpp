@@ -43,4 +43,21 @@ constexpr int kKeyCombNarrow = 16;  // 16 additions, 67 MB per key
 constexpr int kBCombBits = 24;      // 11 additions per [s]B, 11.8 GB (the host harness builds this one)
 constexpr int kBCombFallback = 20;  // 13 additions, 872 MB
 
+// Message i of a launch is msg[off[i] .. off[i] + len[i]) of a buffer of
+// `bytes` bytes.  Every kernel that reads caller messages takes the slice
+// through msg_slice: out of bounds (off > bytes, or len > bytes - off -- no
+// overflow) it gets an empty slice at the buffer's start and ok = 0, and the
+// item is rejected (verification, signing) or gets a zero digest and is counted
+// (SHA-512); the kernel never dereferences the caller's offset.  (Round 4's
+// fault r04e: a key-cache launch read offsets another stream had not written
+// yet, and the wild offset faulted the card.)
+struct MsgSlice {
+  uint64_t off, len;
+  uint32_t ok;
+};
+NT_HD NT_INLINE MsgSlice msg_slice(uint64_t off, uint64_t len, uint64_t bytes) {
+  const uint32_t ok = off <= bytes && len <= bytes - off;
+  return MsgSlice{ok ? off : 0u, ok ? len : 0u, ok};
+}
+
 }  // namespace nt

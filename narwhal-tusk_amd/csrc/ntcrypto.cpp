@@ -85,8 +85,10 @@ constexpr uint64_t kCombHeadroom = 4ull << 30;
 // entry picks the widest width that (a) fits the context's HBM budget on the
 // entry, (b) leaves kCombHeadroom of the device free and (c) hipMalloc grants:
 // 24-bit digits (11 additions per [s]B, 11.8 GB), else 20-bit (13, 872 MB).
+// The fast path reads only the slot's own comb_ready (the entry's
+// fields are written under tables_mu by whichever slot builds the comb first).
 int comb_b_for(Device& dv) {
-  if (dv.d_combB) return NT_OK;
+  if (dv.comb_ready.load(std::memory_order_acquire)) return NT_OK;
   Device& e = *dv.entry;
   std::lock_guard<std::mutex> lk(e.tables_mu);
   if (!e.combB) {
@@ -126,6 +128,7 @@ int comb_b_for(Device& dv) {
   dv.combB = e.combB;
   dv.d_combB = e.d_combB;
   dv.bbits = e.bbits;
+  dv.comb_ready.store(1, std::memory_order_release);
   return NT_OK;
 }
 
@@ -350,7 +353,7 @@ namespace {
 
 // Stage the message span used by items [lo, hi) (rebased offsets, 16-B phase kept).
 int stage_messages(Device& dv, const uint8_t* data, const uint64_t* off, const uint64_t* len,
-                   uint64_t lo, uint64_t hi, uint64_t* base_out) {
+                   uint64_t lo, uint64_t hi, uint64_t* base_out, uint64_t* span_out) {
   uint64_t mn = UINT64_MAX, mx = 0;
   for (uint64_t i = lo; i < hi; ++i) {
     if (len[i] == 0) continue;
@@ -376,6 +379,7 @@ int stage_messages(Device& dv, const uint8_t* data, const uint64_t* off, const u
   NT_TRY(hipMemcpyAsync(dv.d[B_OFF].p, ho, m * 8, hipMemcpyHostToDevice, dv.stream));
   NT_TRY(hipMemcpyAsync(dv.d[B_LEN].p, hl, m * 8, hipMemcpyHostToDevice, dv.stream));
   *base_out = base;
+  *span_out = span;
   return NT_OK;
 }
 
@@ -488,13 +492,42 @@ int msg_copy(Device& dv, const uint8_t* data, const uint64_t* off, const uint64_
   return NT_OK;
 }
 
-// Item counts per chunk in whole rounds R (the signatures one round of resident
-// waves covers, so no launch ends on a nearly empty round): a one-round first
-// chunk so the kernels start after a short copy, then equal whole-round chunks,
-// the last one takes the rest.
+// Item counts per chunk.  A host call is PCIe-bound (config 2: 608 B per
+// verify over a ~48 GB/s link against ~95 verifies per us of kernel), and its
+// copies run back to back on the copy stream, so the call takes about the whole
+// copy plus the kernels that can only start after the LAST copy.  So: a
+// quarter-round first chunk (the first kernel starts after a short copy), whole
+// rounds R in the middle (a launch fills the GPU), and a quarter-round last
+// chunk (the tail after the last copy is one short launch).  NT_PIPE_PLAN=round
+// restores round 4's plan (one-round first chunk, equal whole-round chunks, the
+// rest last) for A/B.
+static bool pipe_plan_round4() {
+  static const bool r4 = [] {
+    const char* e = std::getenv("NT_PIPE_PLAN");
+    return e && std::strcmp(e, "round") == 0;
+  }();
+  return r4;
+}
 std::vector<uint64_t> chunk_targets(uint64_t total, uint64_t R) {
   const uint64_t cap = (uint64_t)pipe_chunks_cap();
   if (cap == 1 || total <= R) return {total};
+  if (!pipe_plan_round4() && cap >= 3) {
+    const uint64_t q = std::max<uint64_t>(64, R / 4 / 64 * 64);
+    std::vector<uint64_t> t{q};
+    // the last chunk starts on a multiple of 64 (every chunk owns whole verdict words)
+    const uint64_t tail = std::max<uint64_t>(q, (total - std::min<uint64_t>(q, total - q)) / 64 * 64);
+    const uint64_t last = total - tail;
+    uint64_t mid_total = tail - q;
+    // whole rounds, grown to whole multiples of R when cap - 2 chunks would not cover it
+    const uint64_t per = std::max<uint64_t>(R, (mid_total + cap - 3) / (cap - 2) + R - 1) / R * R;
+    while (mid_total > 0) {
+      const uint64_t c = std::min(per, mid_total);
+      t.push_back(c);
+      mid_total -= c;
+    }
+    if (last) t.push_back(last);
+    return t;
+  }
   const uint64_t k = std::min<uint64_t>(cap, (total + R - 1) / R);
   const uint64_t mid = ((total - R + k - 2) / (k - 1) + R - 1) / R * R;
   std::vector<uint64_t> t{R};
@@ -655,7 +688,7 @@ int nt_sha512_trunc32(nt_ctx* ctx, const uint8_t* data, const uint64_t* off, con
       NT_TRY(dv.fence((int)c));
       uint64_t ml = 0;  // the chunk's longest message selects the kernel
       for (uint64_t i = lo + a; i < lo + b; ++i) ml = std::max(ml, len[i]);
-      NT_TRY(nt::launch_sha512_trunc32(dv.d[B_DATA].as<uint8_t>(), dv.d[B_OFF].as<uint64_t>() + a,
+      NT_TRY(nt::launch_sha512_trunc32(dv.d[B_DATA].as<uint8_t>(), ms.span, dv.d[B_OFF].as<uint64_t>() + a,
                                        dv.d[B_LEN].as<uint64_t>() + a, b - a, dv.d[B_OUT].as<uint8_t>() + 32 * a,
                                        dv.cstr((int)c), ml));
     }
@@ -700,7 +733,7 @@ int nt_ed25519_verify_strict(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* si
                             hipMemcpyHostToDevice, dv.cstream));
       NT_TRY(dv.fence((int)c));
       NT_CHK(dv.verify_chunk((int)c, NT_MODE_STRICT, dv.d[B_PK].as<uint8_t>() + 32 * a,
-                             dv.d[B_SIG].as<uint8_t>() + 64 * a, dv.d[B_DATA].as<uint8_t>(),
+                             dv.d[B_SIG].as<uint8_t>() + 64 * a, dv.d[B_DATA].as<uint8_t>(), ms.span,
                              dv.d[B_OFF].as<uint64_t>() + a, dv.d[B_LEN].as<uint64_t>() + a, b - a,
                              dv.d[B_OUT].as<uint64_t>() + a / 64));
     }
@@ -852,12 +885,12 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
           void* st = (c & 1) ? dv.stash2.p : dv.d[B_STASH].p;
           void* so = (c & 1) ? dv.sort2.p : dv.d[B_SORT].p;
           NT_CHK(dv.keyset_launch(s, st, [&] {
-            return nt::launch_verify_keyset(NT_MODE_COFACTORLESS, ks->bits, (const uint32_t*)dk, dsig, dmsg, doff, dlen,
-                                            mc, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, dv.bbits, st, so,
+            return nt::launch_verify_keyset(NT_MODE_COFACTORLESS, ks->bits, (const uint32_t*)dk, dsig, dmsg,
+                                            32 * (g1 - g0), doff, dlen, mc, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, dv.bbits, st, so,
                                             dout, dv.cus, s);
           }));
         } else {
-          NT_CHK(dv.verify_chunk((int)c, NT_MODE_COFACTORLESS, dk, dsig, dmsg, doff, dlen, mc, dout));
+          NT_CHK(dv.verify_chunk((int)c, NT_MODE_COFACTORLESS, dk, dsig, dmsg, 32 * (g1 - g0), doff, dlen, mc, dout));
         }
       }
       NT_TRY(nt::launch_group_and(dv.d[B_FIRST].as<uint64_t>() + gl, dv.d[B_CNT].as<uint32_t>() + gl, g1 - g0, dout,
@@ -922,9 +955,10 @@ int nt_ed25519_sign_batch(nt_ctx* ctx, const uint8_t* seed32, const uint8_t* msg
     const uint64_t m = hi - lo;
     const uint8_t* d_msg = nullptr;
     const uint64_t *d_off = nullptr, *d_len = nullptr;
+    uint64_t span = 0;
     if (sig64) {
       uint64_t base;
-      NT_CHK(stage_messages(dv, msg, off, len, lo, hi, &base));
+      NT_CHK(stage_messages(dv, msg, off, len, lo, hi, &base, &span));
       d_msg = dv.d[B_DATA].as<uint8_t>();
       d_off = dv.d[B_OFF].as<uint64_t>();
       d_len = dv.d[B_LEN].as<uint64_t>();
@@ -933,7 +967,7 @@ int nt_ed25519_sign_batch(nt_ctx* ctx, const uint8_t* seed32, const uint8_t* msg
     NT_CHK(dv.d[B_SIG].ensure(m * 64));
     NT_CHK(dv.d[B_OUT].ensure(m * 32));
     NT_TRY(hipMemcpyAsync(dv.d[B_OUT].p, seed32 + 32 * lo, m * 32, hipMemcpyHostToDevice, dv.stream));
-    NT_TRY(nt::launch_sign(dv.d[B_OUT].as<uint8_t>(), d_msg, d_off, d_len, m, dv.d_combB, dv.bbits,
+    NT_TRY(nt::launch_sign(dv.d[B_OUT].as<uint8_t>(), d_msg, span, d_off, d_len, m, dv.d_combB, dv.bbits,
                            dv.d[B_PK].as<uint8_t>(), sig64 ? dv.d[B_SIG].as<uint8_t>() : nullptr,
                            dv.sign_blocks, dv.stream));
     NT_TRY(hipMemcpyAsync(pk32 + 32 * lo, dv.d[B_PK].p, m * 32, hipMemcpyDeviceToHost, dv.stream));
@@ -1112,7 +1146,7 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
       hipStream_t s = dv.cstr((int)c);
       NT_CHK(dv.keyset_launch(s, st, [&] {
         return nt::launch_verify_keyset(mode, ks->bits, dv.d[B_PK].as<uint32_t>() + a,
-                                        dv.d[B_SIG].as<uint8_t>() + 64 * a, dv.d[B_DATA].as<uint8_t>(),
+                                        dv.d[B_SIG].as<uint8_t>() + 64 * a, dv.d[B_DATA].as<uint8_t>(), ms.span,
                                         dv.d[B_OFF].as<uint64_t>() + a, dv.d[B_LEN].as<uint64_t>() + a, b - a,
                                         pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, dv.bbits, st, so,
                                         dv.d[B_OUT].as<uint64_t>() + a / 64, dv.cus, s);
@@ -1146,39 +1180,39 @@ int nt_ed25519_verify_batch_groups_keyset(nt_ctx* ctx, const nt_keyset* ks, cons
 }
 
 // ---- device-resident entry points ---------------------------------------
-int nt_dev_sha512_trunc32(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_data,
-                          const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
+// `stream` is the caller's; NULL is HIP's NULL stream (not the library's), so a
+// caller whose inputs come from work on the NULL stream is ordered after it.
+int nt_dev_sha512_trunc32(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_data, uint64_t data_bytes,
+                          const uint64_t* d_off, const uint64_t* d_len, uint64_t n, uint32_t* d_bad,
                           uint8_t* d_out32) {
   Device* dv = dev_of(ctx, dev);
-  if (!dv) return NT_EINVAL;
+  if (!dv || (n && (!d_data || !d_off || !d_len || !d_out32))) return NT_EINVAL;
   NT_TRY(hipSetDevice(dv->ordinal));
-  hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
-  NT_TRY(nt::launch_sha512_trunc32(d_data, d_off, d_len, n, d_out32, s));
+  NT_TRY(nt::launch_sha512_trunc32(d_data, data_bytes, d_off, d_len, n, d_out32, (hipStream_t)stream, ~0ull, d_bad));
   return NT_OK;
 }
 
-int nt_dev_sha512_trunc32_bounded(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_data,
+int nt_dev_sha512_trunc32_bounded(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_data, uint64_t data_bytes,
                                   const uint64_t* d_off, const uint64_t* d_len, uint64_t n, uint64_t max_len,
-                                  int prio, uint8_t* d_out32) {
+                                  uint32_t* d_bad, uint8_t* d_out32) {
   Device* dv = dev_of(ctx, dev);
-  if (!dv || prio > 3) return NT_EINVAL;
+  if (!dv || (n && (!d_data || !d_off || !d_len || !d_out32))) return NT_EINVAL;
   NT_TRY(hipSetDevice(dv->ordinal));
-  hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
-  NT_TRY(nt::launch_sha512_trunc32(d_data, d_off, d_len, n, d_out32, s, max_len, prio));
+  NT_TRY(nt::launch_sha512_trunc32(d_data, data_bytes, d_off, d_len, n, d_out32, (hipStream_t)stream, max_len, d_bad));
   return NT_OK;
 }
 
 int nt_dev_ed25519_verify(nt_ctx* ctx, int dev, void* stream, int mode, const uint8_t* d_pk32,
-                          const uint8_t* d_sig64, const uint8_t* d_msg, const uint64_t* d_off,
+                          const uint8_t* d_sig64, const uint8_t* d_msg, uint64_t msg_bytes, const uint64_t* d_off,
                           const uint64_t* d_len, uint64_t n, uint64_t* d_out_words) {
   Device* dv = dev_of(ctx, dev);
   if (!dv || (mode != NT_MODE_STRICT && mode != NT_MODE_COFACTORLESS)) return NT_EINVAL;
+  if (n && (!d_pk32 || !d_sig64 || !d_msg || !d_off || !d_len || !d_out_words)) return NT_EINVAL;
   NT_TRY(hipSetDevice(dv->ordinal));
-  hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
   // the [k]A workspaces are per device: launches that use one are ordered by its event
   std::lock_guard<std::mutex> lk(dv->mu);
   NT_CHK(verify_tables(*dv));
-  NT_TRY(dv->verify_dev(mode, d_pk32, d_sig64, d_msg, d_off, d_len, n, d_out_words, s));
+  NT_TRY(dv->verify_dev(mode, d_pk32, d_sig64, d_msg, msg_bytes, d_off, d_len, n, d_out_words, (hipStream_t)stream));
   return NT_OK;
 }
 
@@ -1188,20 +1222,20 @@ int nt_dev_group_and(nt_ctx* ctx, int dev, void* stream, const uint64_t* d_first
   Device* dv = dev_of(ctx, dev);
   if (!dv) return NT_EINVAL;
   NT_TRY(hipSetDevice(dv->ordinal));
-  hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
-  NT_TRY(nt::launch_group_and(d_first, d_cnt, G, d_sig_words, d_group_words, s));
+  NT_TRY(nt::launch_group_and(d_first, d_cnt, G, d_sig_words, d_group_words, (hipStream_t)stream));
   return NT_OK;
 }
 
 int nt_dev_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int dev, void* stream, int mode,
                                  const uint32_t* d_key_idx, const uint8_t* d_sig64, const uint8_t* d_msg,
-                                 const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
+                                 uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
                                  uint64_t* d_out_words) {
   Device* dv = dev_of(ctx, dev);
   if (!dv || !ks || ks->ctx != ctx || (mode != NT_MODE_STRICT && mode != NT_MODE_COFACTORLESS && mode != NT_MODE_MIXED))
     return NT_EINVAL;
+  if (n && (!d_key_idx || !d_sig64 || !d_msg || !d_off || !d_len || !d_out_words)) return NT_EINVAL;
   NT_TRY(hipSetDevice(dv->ordinal));
-  hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
+  hipStream_t s = (hipStream_t)stream;
   const auto& pd = ks->t->dev[dev];
   // the device's two stashes, shared with the host entry points, each ordered
   // against every other user by its event whatever the streams; successive
@@ -1214,22 +1248,23 @@ int nt_dev_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int dev, void
   void* stash = k ? dv->stash2.p : dv->d[B_STASH].p;
   void* so = k ? dv->sort2.p : dv->d[B_SORT].p;
   return dv->keyset_launch(s, stash, [&] {
-    return nt::launch_verify_keyset(mode, ks->bits, d_key_idx, d_sig64, d_msg, d_off, d_len, n, pd.d_meta, pd.d_enc,
-                                    pd.d_comb, ks->nkeys, dv->d_combB, dv->bbits, stash, so, d_out_words, dv->cus, s);
+    return nt::launch_verify_keyset(mode, ks->bits, d_key_idx, d_sig64, d_msg, msg_bytes, d_off, d_len, n, pd.d_meta,
+                                    pd.d_enc, pd.d_comb, ks->nkeys, dv->d_combB, dv->bbits, stash, so, d_out_words,
+                                    dv->cus, s);
   });
 }
 
-int nt_dev_ed25519_sign(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_seed32,
-                        const uint8_t* d_msg, const uint64_t* d_off, const uint64_t* d_len,
-                        uint64_t n, uint8_t* d_pk32, uint8_t* d_sig64) {
+int nt_dev_ed25519_sign(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_seed32, const uint8_t* d_msg,
+                        uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
+                        uint8_t* d_pk32, uint8_t* d_sig64) {
   Device* dv = dev_of(ctx, dev);
-  if (!dv) return NT_EINVAL;
+  if (!dv || (n && (!d_seed32 || !d_pk32))) return NT_EINVAL;
+  if (n && d_sig64 && (!d_msg || !d_off || !d_len)) return NT_EINVAL;
   NT_TRY(hipSetDevice(dv->ordinal));
-  hipStream_t s = stream ? (hipStream_t)stream : dv->stream;
   std::lock_guard<std::mutex> lk(dv->mu);
   NT_CHK(comb_b_for(*dv));
-  NT_TRY(nt::launch_sign(d_seed32, d_msg, d_off, d_len, n, dv->d_combB, dv->bbits, d_pk32, d_sig64,
-                         dv->sign_blocks, s));
+  NT_TRY(nt::launch_sign(d_seed32, d_sig64 ? d_msg : nullptr, msg_bytes, d_off, d_len, n, dv->d_combB, dv->bbits,
+                         d_pk32, d_sig64, dv->sign_blocks, (hipStream_t)stream));
   return NT_OK;
 }
 

@@ -125,25 +125,23 @@ struct Budget {
   }
 };
 
-// The device entry's two compute streams.  HIP multiplexes a process's
-// streams over GPU_MAX_HW_QUEUES (4) queues per priority and hands a new stream
-// the least-used one, so two streams can share a queue, and then their kernels
-// run strictly in order.  NT_STREAMS selects the kind: mask (default: a CU
-// mask enabling every CU -- a masked stream gets a queue of its own, so the
-// library's streams leave the shared queues to the caller's), plain (may share
-// a queue; NT_SHARED_QUEUES=1 too), prio (the second stream at the highest
-// priority: HIP keeps a queue pool per priority).  Measured (one box, two
-// rounds each; profiles/r04/ab_streams.txt): with the mask, a caller
-// pipelining on its own (torch) streams gets config 3 at 12.6 M/s and config
-// 2's two-stream line at 101.9 M/s; with plain library streams 12.6 and 96.5
-// (the caller's two streams no longer overlap).
+// The device entry's two compute streams.  Default: plain non-blocking
+// streams (ordered against no other stream, the NULL stream included -- ADVICE
+// r04: a CU-masked stream is a BLOCKING stream, so every launch on it waited
+// for, and held up, work on the NULL stream of the whole process).  HIP
+// multiplexes a process's streams over GPU_MAX_HW_QUEUES (4) queues per
+// priority and hands a new stream the least-used one, so the two may share a
+// hardware queue with other streams of the process; NT_STREAMS=mask gives each
+// one a queue of its own (a CU mask enabling every CU: a masked stream never
+// shares its queue) at the price of NULL-stream ordering, NT_STREAMS=prio puts
+// the second at the highest priority.  Measured (profiles/r04/ab_streams.txt,
+// profiles/r05/): the kinds give the same rates when the pipelined steps run on
+// the library's streams.
 inline hipError_t compute_stream(hipStream_t* s, uint32_t cus, int which) {
   static const int kind = [] {
-    const char* q = std::getenv("NT_SHARED_QUEUES");
-    if (q && *q == '1') return 1;
     const char* e = std::getenv("NT_STREAMS");
-    if (!e) return 0;
-    return std::strcmp(e, "plain") == 0 ? 1 : std::strcmp(e, "prio") == 0 ? 2 : 0;
+    if (!e) return 1;
+    return std::strcmp(e, "mask") == 0 ? 0 : std::strcmp(e, "prio") == 0 ? 2 : 1;
   }();
   if (kind == 1 || (kind == 2 && which == 0)) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
   if (kind == 2) {
@@ -167,6 +165,7 @@ struct Device {
   hipStream_t stream = nullptr;
   uint32_t* d_combB = nullptr;  // wide comb of B (verify, key-cache verify, sign): comb_b_for() sets it
   int bbits = 0;                // its digit width (nt::kBCombBits or nt::kBCombFallback)
+  std::atomic<int> comb_ready{0};  // this slot's d_combB / bbits are set (comb_b_for's lock-free fast path)
   void* d_ws = nullptr;         // verify workspace: ensure_ws() on the first verify
   uint32_t ws_slots = 0;
   uint32_t sign_blocks = 0;
@@ -331,15 +330,16 @@ struct Device {
 
   // verify launch of chunk c: even chunks use the device workspace on `stream`,
   // odd chunks stream2's own workspace (grown to the chunk's grid)
-  int verify_chunk(int c, int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+  int verify_chunk(int c, int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint64_t msg_bytes,
                    const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out) {
-    if (!(c & 1)) return verify(mode, pk, sig, msg, off, len, n, out, stream) == hipSuccess ? NT_OK : NT_EHIP;
+    if (!(c & 1))
+      return verify(mode, pk, sig, msg, msg_bytes, off, len, n, out, stream) == hipSuccess ? NT_OK : NT_EHIP;
     const uint64_t blocks = nt::verify_grid(n, ws_slots);
     const int rc = grow_ws2(blocks);
     if (rc != NT_OK) return rc;
     if (hipStreamWaitEvent(stream2, ws2_done, 0) != hipSuccess ||
-        nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, bbits, ws2.p, (uint32_t)std::max<uint64_t>(blocks, 1),
-                          out, stream2) != hipSuccess ||
+        nt::launch_verify(mode, pk, sig, msg, msg_bytes, off, len, n, d_combB, bbits, ws2.p,
+                          (uint32_t)std::max<uint64_t>(blocks, 1), out, stream2) != hipSuccess ||
         hipEventRecord(ws2_done, stream2) != hipSuccess)
       return NT_EHIP;
     return NT_OK;
@@ -390,24 +390,23 @@ struct Device {
   // issued on two caller streams overlap -- the waves of the next batch fill the
   // SIMDs the previous batch's last round leaves idle.  Calls on one stream stay
   // in stream order.  (Caller holds mu.)
-  hipError_t verify_dev(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
+  hipError_t verify_dev(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint64_t msg_bytes,
                         const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out, hipStream_t s) {
-    if ((dev_calls++ & 1u) == 0) return verify(mode, pk, sig, msg, off, len, n, out, s);
+    if ((dev_calls++ & 1u) == 0) return verify(mode, pk, sig, msg, msg_bytes, off, len, n, out, s);
     if (grow_ws2(ws_slots) != NT_OK) return hipErrorOutOfMemory;
     hipError_t e = hipStreamWaitEvent(s, ws2_done, 0);
     if (e != hipSuccess) return e;
-    e = nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, bbits, ws2.p, ws_slots, out, s);
+    e = nt::launch_verify(mode, pk, sig, msg, msg_bytes, off, len, n, d_combB, bbits, ws2.p, ws_slots, out, s);
     if (e != hipSuccess) return e;
     return hipEventRecord(ws2_done, s);
   }
 
   // verify launch that shares the workspace: wait for the previous user, then mark
-  hipError_t verify(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg,
-                    const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out,
-                    hipStream_t s) {
+  hipError_t verify(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint64_t msg_bytes,
+                    const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out, hipStream_t s) {
     hipError_t e = hipStreamWaitEvent(s, ws_done, 0);
     if (e != hipSuccess) return e;
-    e = nt::launch_verify(mode, pk, sig, msg, off, len, n, d_combB, bbits, d_ws, ws_slots, out, s);
+    e = nt::launch_verify(mode, pk, sig, msg, msg_bytes, off, len, n, d_combB, bbits, d_ws, ws_slots, out, s);
     if (e != hipSuccess) return e;
     return hipEventRecord(ws_done, s);
   }

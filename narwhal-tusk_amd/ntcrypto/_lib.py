@@ -74,13 +74,12 @@ def load_library(path=None):
     lib.nt_ed25519_verify_batch_groups.argtypes = [_vp, _u8p, _u8p, _u64p, _u32p, _u8p, _u64, _u8p, _u8p]
     lib.nt_ed25519_sign_batch.argtypes = [_vp, _u8p, _u8p, _u64p, _u64p, _u64, _u8p, _u8p]
     lib.nt_ed25519_keypair_batch.argtypes = [_vp, _u8p, _u64, _u8p]
-    lib.nt_dev_sha512_trunc32.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, _u64, _vp]
-    lib.nt_dev_sha512_trunc32_bounded.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, _u64, _u64, ctypes.c_int,
-                                                  _vp]
-    lib.nt_dev_ed25519_verify.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_int, _vp, _vp, _vp, _vp, _vp,
+    lib.nt_dev_sha512_trunc32.argtypes = [_vp, ctypes.c_int, _vp, _vp, _u64, _vp, _vp, _u64, _vp, _vp]
+    lib.nt_dev_sha512_trunc32_bounded.argtypes = [_vp, ctypes.c_int, _vp, _vp, _u64, _vp, _vp, _u64, _u64, _vp, _vp]
+    lib.nt_dev_ed25519_verify.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_int, _vp, _vp, _vp, _u64, _vp, _vp,
                                           _u64, _vp]
     lib.nt_dev_group_and.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _u64, _vp, _vp]
-    lib.nt_dev_ed25519_sign.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp]
+    lib.nt_dev_ed25519_sign.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, _u64, _vp, _vp, _u64, _vp, _vp]
     lib.nt_keyset_create.argtypes = [_vp, _u8p, ctypes.c_uint32, ctypes.POINTER(_vp)]
     lib.nt_keyset_free.argtypes = [_vp]
     lib.nt_keyset_free.restype = None
@@ -89,8 +88,8 @@ def load_library(path=None):
     lib.nt_ed25519_verify_keyset.argtypes = [_vp, _vp, ctypes.c_int, _u32p, _u8p, _u8p, _u64p, _u64p, _u64, _u8p]
     lib.nt_ed25519_verify_batch_groups_keyset.argtypes = [_vp, _vp, _u32p, _u8p, _u64p, _u32p, _u8p, _u64, _u8p,
                                                           _u8p]
-    lib.nt_dev_ed25519_verify_keyset.argtypes = [_vp, _vp, ctypes.c_int, _vp, ctypes.c_int, _vp, _vp, _vp, _vp,
-                                                 _vp, _u64, _vp]
+    lib.nt_dev_ed25519_verify_keyset.argtypes = [_vp, _vp, ctypes.c_int, _vp, ctypes.c_int, _vp, _vp, _vp, _u64,
+                                                 _vp, _vp, _u64, _vp]
     lib.nt_set_small_call_path.argtypes = [_vp, ctypes.c_int, ctypes.c_int]
     lib.nt_call_counts.argtypes = [_vp, _u64p, _u64p]
     if hasattr(lib, "nt_small_call_model"):  # absent from older A/B builds (NTCRYPTO_LIB)
@@ -134,6 +133,12 @@ def _torch_first():
     torch = sys.modules.get("torch")
     if torch is not None and torch.cuda.is_available() and not torch.cuda.is_initialized():
         torch.cuda.init()
+
+
+def nbytes(t):
+    """Byte size of a device buffer given as a torch tensor (the msg_bytes /
+    data_bytes argument of the device-resident entry points)."""
+    return int(t.numel()) * int(t.element_size())
 
 
 class Backend:
@@ -212,7 +217,7 @@ class Backend:
 
     def dev_stream(self, dev=0, which=0):
         """Raw hipStream_t of device entry `dev`'s compute stream `which` (0 / 1):
-        the two sit on hardware queues of their own (nt_dev_stream)."""
+        the streams the host entry points pipeline on (nt_dev_stream)."""
         p = _vp()
         _check(self.lib.nt_dev_stream(self.ctx, int(dev), int(which), ctypes.byref(p)), "nt_dev_stream")
         return int(p.value)
@@ -293,25 +298,28 @@ class Backend:
     def keyset(self, pks):
         return Keyset(self, pks)
 
-    # ---- device-resident (torch tensors or raw pointers) ----
-    def dev_verify(self, dev, stream, mode, d_pk, d_sig, d_msg, d_off, d_len, n, d_out):
-        _check(self.lib.nt_dev_ed25519_verify(self.ctx, dev, stream, mode, d_pk, d_sig, d_msg, d_off, d_len,
-                                              n, d_out), "nt_dev_ed25519_verify")
+    # ---- device-resident (raw device pointers; stream 0 = HIP's NULL stream) ----
+    # Message buffers come with their byte size, as in the C ABI: an item whose
+    # slice d_msg[off, off + len) lies outside [0, msg_bytes) is never read.
+    def dev_verify(self, dev, stream, mode, d_pk, d_sig, d_msg, msg_bytes, d_off, d_len, n, d_out):
+        _check(self.lib.nt_dev_ed25519_verify(self.ctx, dev, stream, mode, d_pk, d_sig, d_msg, int(msg_bytes), d_off,
+                                              d_len, n, d_out), "nt_dev_ed25519_verify")
 
-    def dev_sha512(self, dev, stream, d_data, d_off, d_len, n, d_out, max_len=None, prio=None):
+    def dev_sha512(self, dev, stream, d_data, data_bytes, d_off, d_len, n, d_out, max_len=None, d_bad=None):
         """max_len: an upper bound of the message lengths, if known (selects the
-        kernel); prio: wave issue priority 0..3 (nt_dev_sha512_trunc32_bounded)"""
-        if max_len is None and prio is None:
-            _check(self.lib.nt_dev_sha512_trunc32(self.ctx, dev, stream, d_data, d_off, d_len, n, d_out),
-                   "nt_dev_sha512_trunc32")
+        kernel: nt_dev_sha512_trunc32_bounded); d_bad: device uint32 counter of
+        out-of-bounds items (zero digests), or None"""
+        if max_len is None:
+            _check(self.lib.nt_dev_sha512_trunc32(self.ctx, dev, stream, d_data, int(data_bytes), d_off, d_len, n,
+                                                  d_bad, d_out), "nt_dev_sha512_trunc32")
         else:
-            _check(self.lib.nt_dev_sha512_trunc32_bounded(
-                self.ctx, dev, stream, d_data, d_off, d_len, n, (1 << 64) - 1 if max_len is None else int(max_len),
-                -1 if prio is None else int(prio), d_out), "nt_dev_sha512_trunc32_bounded")
+            _check(self.lib.nt_dev_sha512_trunc32_bounded(self.ctx, dev, stream, d_data, int(data_bytes), d_off, d_len,
+                                                          n, int(max_len), d_bad, d_out),
+                   "nt_dev_sha512_trunc32_bounded")
 
-    def dev_sign(self, dev, stream, d_seed, d_msg, d_off, d_len, n, d_pk, d_sig):
-        _check(self.lib.nt_dev_ed25519_sign(self.ctx, dev, stream, d_seed, d_msg, d_off, d_len, n, d_pk, d_sig),
-               "nt_dev_ed25519_sign")
+    def dev_sign(self, dev, stream, d_seed, d_msg, msg_bytes, d_off, d_len, n, d_pk, d_sig):
+        _check(self.lib.nt_dev_ed25519_sign(self.ctx, dev, stream, d_seed, d_msg, int(msg_bytes), d_off, d_len, n,
+                                            d_pk, d_sig), "nt_dev_ed25519_sign")
 
     def dev_group_and(self, dev, stream, d_first, d_cnt, G, d_sig_words, d_group_words):
         _check(self.lib.nt_dev_group_and(self.ctx, dev, stream, d_first, d_cnt, G, d_sig_words, d_group_words),
@@ -385,9 +393,9 @@ class Keyset:
             return _unpack(gb, G), _unpack(sb, nsig)
         return _unpack(gb, G)
 
-    def dev_verify(self, dev, stream, mode, d_key_idx, d_sig, d_msg, d_off, d_len, n, d_out):
+    def dev_verify(self, dev, stream, mode, d_key_idx, d_sig, d_msg, msg_bytes, d_off, d_len, n, d_out):
         _check(self.be.lib.nt_dev_ed25519_verify_keyset(self.be.ctx, self.h, dev, stream, mode, d_key_idx, d_sig,
-                                                        d_msg, d_off, d_len, n, d_out),
+                                                        d_msg, int(msg_bytes), d_off, d_len, n, d_out),
                "nt_dev_ed25519_verify_keyset")
 
 

@@ -230,6 +230,23 @@ int nth_verify(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* m
   else verify_n<kCofactorless, 1>(ok, Ap, Sp, Mp, Lp, at, bcomb());
   return (int)ok[0];
 }
+// The message bound of every kernel that reads caller messages (nt_common.hpp
+// msg_slice): out3 = {off, len, ok} as the kernel takes the slice.
+void nth_msg_slice(uint64_t off, uint64_t len, uint64_t bytes, uint64_t* out3) {
+  const MsgSlice ms = msg_slice(off, len, bytes);
+  out3[0] = ms.off;
+  out3[1] = ms.len;
+  out3[2] = ms.ok;
+}
+// One item of k_ed25519_verify's body: the slice of a `bytes`-byte message
+// buffer, then the verification, the verdict ANDed with the bound (the kernel's
+// act & ok).  An out-of-bounds slice is never read: the harness hands the
+// arithmetic the clamped (empty) slice, exactly as the kernel does.
+int nth_verify_item(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint64_t bytes,
+                    uint64_t off, uint64_t len) {
+  const MsgSlice ms = msg_slice(off, len, bytes);
+  return nth_verify(mode, pk, sig, msg + ms.off, ms.len) & (int)ms.ok;
+}
 // verify_uv with the trivial lattice vector (u, v) = (k, 1), 253-bit ladder:
 // the path sc_halfsize falls back to, checked against the same corpus.
 int nth_verify_trivial(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint64_t len) {

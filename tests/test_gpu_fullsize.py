@@ -20,6 +20,12 @@ import types
 import numpy as np
 import pytest
 
+
+def nbytes(t):
+    """byte size of a device tensor: the msg_bytes argument of the nt_dev_* entry points"""
+    return int(t.numel()) * int(t.element_size())
+
+
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -54,7 +60,7 @@ def test_cfg2_million_verifies(env):
         ln = torch.full((n,), L, dtype=torch.int64, device=dev)
         pk = torch.empty((n, 32), dtype=torch.uint8, device=dev)
         sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
-    be.dev_sign(0, sp, seeds.data_ptr(), msgs.data_ptr(), off.data_ptr(), ln.data_ptr(), n, pk.data_ptr(),
+    be.dev_sign(0, sp, seeds.data_ptr(), msgs.data_ptr(), nbytes(msgs), off.data_ptr(), ln.data_ptr(), n, pk.data_ptr(),
                 sig.data_ptr())
     torch.cuda.synchronize(dev)
 
@@ -84,7 +90,7 @@ def test_cfg2_million_verifies(env):
     runs = []
     for _ in range(2):
         out = torch.zeros(words, dtype=torch.int64, device=dev)
-        be.dev_verify(0, sp, env.ntcrypto.NT_MODE_STRICT, pk.data_ptr(), sig.data_ptr(), msgs.data_ptr(),
+        be.dev_verify(0, sp, env.ntcrypto.NT_MODE_STRICT, pk.data_ptr(), sig.data_ptr(), msgs.data_ptr(), nbytes(msgs),
                       off.data_ptr(), ln.data_ptr(), n, out.data_ptr())
         torch.cuda.synchronize(dev)
         runs.append(_bits(torch, out, n))
@@ -121,7 +127,7 @@ def test_cfg4_sha512_full_size(env):
         out0 = torch.empty((m, 32), dtype=torch.uint8, device=dev)
         out1 = torch.empty((m, 32), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize(dev)
-    be.dev_sha512(0, sp, data.data_ptr(), off.data_ptr(), ln.data_ptr(), m, out0.data_ptr())
+    be.dev_sha512(0, sp, data.data_ptr(), nbytes(data), off.data_ptr(), ln.data_ptr(), m, out0.data_ptr())
     torch.cuda.synchronize(dev)
     rng = np.random.default_rng(3)
     idx = np.unique(np.concatenate([[0, 63, 64, m - 1], rng.integers(0, m, 12)]))
@@ -133,7 +139,7 @@ def test_cfg4_sha512_full_size(env):
     j, k = int(rng.integers(0, m)), int(rng.integers(0, ml))
     data[j * ml + k] ^= 0x5A
     torch.cuda.synchronize(dev)
-    be.dev_sha512(0, sp, data.data_ptr(), off.data_ptr(), ln.data_ptr(), m, out1.data_ptr())
+    be.dev_sha512(0, sp, data.data_ptr(), nbytes(data), off.data_ptr(), ln.data_ptr(), m, out1.data_ptr())
     torch.cuda.synchronize(dev)
     d1 = out1.cpu().numpy()
     changed = np.nonzero((d0 != d1).any(axis=1))[0]
@@ -185,8 +191,8 @@ def test_sha512_bounded_hint_selects_kernel_not_result(env):
     """nt_dev_sha512_trunc32_bounded: max_len only selects the kernel (one-lane
     below 16 KB, the two-wave pipe above, for launches of <= 32,768 messages):
     digests equal hashlib whatever the hint says -- a right bound, a bound
-    below some lengths (a wrong hint) and no hint, at wave priorities 0..3 --
-    over lengths around every padding edge and across the 16 KB switch."""
+    below some lengths (a wrong hint) and no hint -- over lengths around every
+    padding edge and across the 16 KB switch."""
     torch, be, dev, sp = env.torch, env.be, env.dev, env.sp
     rng = np.random.default_rng(16)
     lens = [0, 1, 72, 111, 112, 127, 128, 129, 239, 240, 3336, 16383, 16384, 16385, 40000]
@@ -200,10 +206,10 @@ def test_sha512_bounded_hint_selects_kernel_not_result(env):
         o = torch.from_numpy(off).to(dev)
         ln = torch.tensor(lens, dtype=torch.int64, device=dev)
     torch.cuda.synchronize(dev)
-    for hint, prio in ((None, None), (max(lens), None), (4096, 3), (72, 0), (None, 1)):
+    for hint in (None, max(lens), 4096, 72):
         out = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
         torch.cuda.synchronize(dev)
-        be.dev_sha512(0, sp, d.data_ptr(), o.data_ptr(), ln.data_ptr(), n, out.data_ptr(), max_len=hint, prio=prio)
+        be.dev_sha512(0, sp, d.data_ptr(), nbytes(d), o.data_ptr(), ln.data_ptr(), n, out.data_ptr(), max_len=hint)
         torch.cuda.synchronize(dev)
         got = out.cpu().numpy()
         bad = [i for i in range(n) if got[i].tobytes() != want[i]]

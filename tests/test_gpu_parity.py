@@ -11,6 +11,12 @@ import pytest
 
 from _oracle import expand
 
+
+def nbytes(t):
+    """byte size of a device tensor: the msg_bytes argument of the nt_dev_* entry points"""
+    return int(t.numel()) * int(t.element_size())
+
+
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 pytestmark = pytest.mark.gpu
 
@@ -401,7 +407,7 @@ def test_verify_ragged_message_lengths(be, oracle):
     out = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
     st = torch.cuda.Stream(dev)
     be.dev_verify(0, st.cuda_stream, ntcrypto.NT_MODE_COFACTORLESS, t["pk"].data_ptr(), t["sig"].data_ptr(),
-                  t["data"].data_ptr(), t["off"].data_ptr(), t["len"].data_ptr(), n, out.data_ptr())
+                  t["data"].data_ptr(), nbytes(t["data"]), t["off"].data_ptr(), t["len"].data_ptr(), n, out.data_ptr())
     torch.cuda.synchronize(dev)
     cof = np.unpackbits(out.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
     assert np.array_equal(cof, ~flip)
@@ -444,9 +450,82 @@ def test_keyset_device_api_two_launches(be, corpus, monkeypatch):
     out = torch.zeros((n + 63) // 64 + 1, dtype=torch.int64, device=dev)
     st = torch.cuda.Stream(dev)
     ks.dev_verify(0, st.cuda_stream, ntcrypto.NT_MODE_MIXED, t["k"].data_ptr(), t["sig"].data_ptr(),
-                  t["msg"].data_ptr(), t["off"].data_ptr(), t["len"].data_ptr(), n, out.data_ptr())
+                  t["msg"].data_ptr(), nbytes(t["msg"]), t["off"].data_ptr(), t["len"].data_ptr(), n, out.data_ptr())
     st.synchronize()
     got = np.unpackbits(out.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
     assert n > (8 << 20)
     assert int((got != want).sum()) == 0
     ks.close()
+
+
+def test_device_api_out_of_bounds_items(be, corpus):
+    """the nt_dev_* entry points take the message buffer's
+    byte size and never read outside it.  The corpus's honest entries (all
+    accept) with a quarter of their offsets / lengths pushed out of the buffer
+    -- past the end, 2^62 away, a length that wraps 64 bits, a slice that ends
+    one byte past the end: those items are rejected by verify_strict and the key
+    cache (mixed mode, strict bit set), get a zero digest and are counted by
+    SHA-512, get an all-zero signature from signing; every other item is
+    unchanged (verdicts, digests and signatures equal to the in-bounds run)."""
+    import ntcrypto
+    import torch
+    dev = torch.device("cuda", 0)
+    honest = np.flatnonzero(corpus["strict"].astype(bool))
+    assert len(honest) >= 16
+    pick = np.resize(honest, 256)
+    n = len(pick)
+    msg = np.ascontiguousarray(corpus["msg"])
+    nbm = len(msg)
+    off = corpus["off"][pick].astype(np.uint64)
+    ln = corpus["len"][pick].astype(np.uint64)
+    bad = np.zeros(n, bool)
+    bad[3::4] = True
+    boff, bln = off.copy(), ln.copy()
+    kinds = [(nbm + 1, 0), (1 << 62, 8), (64, (1 << 64) - 40), (nbm - 7, 8)]
+    for j, i in enumerate(np.flatnonzero(bad)):
+        o, l = kinds[j % len(kinds)]
+        boff[i], bln[i] = o, l
+    uniq, inv = np.unique(corpus["pk"][pick], axis=0, return_inverse=True)
+    ks = be.keyset(uniq)
+    t = {"pk": torch.from_numpy(np.ascontiguousarray(corpus["pk"][pick])).to(dev),
+         "sig": torch.from_numpy(np.ascontiguousarray(corpus["sig"][pick])).to(dev),
+         "msg": torch.from_numpy(msg).to(dev),
+         "k": torch.from_numpy((inv.ravel().astype(np.uint32) | np.uint32(ntcrypto.NT_KEY_STRICT_BIT)).view(np.int32)).to(dev),
+         "seed": torch.from_numpy(np.resize(np.arange(32, dtype=np.uint8), (n, 32)).copy()).to(dev)}
+    for name, o, l in (("good", off, ln), ("bad", boff, bln)):
+        t["off_" + name] = torch.from_numpy(o.view(np.int64)).to(dev)
+        t["len_" + name] = torch.from_numpy(l.view(np.int64)).to(dev)
+    st = torch.cuda.Stream(dev)
+    res = {}
+    for name in ("good", "bad"):
+        o, l = t["off_" + name].data_ptr(), t["len_" + name].data_ptr()
+        v = torch.zeros(n // 64 + 1, dtype=torch.int64, device=dev)
+        kv = torch.zeros(n // 64 + 1, dtype=torch.int64, device=dev)
+        dg = torch.full((n, 32), 0xAB, dtype=torch.uint8, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        spk = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        ssig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
+        with torch.cuda.stream(st):
+            be.dev_verify(0, st.cuda_stream, ntcrypto.NT_MODE_STRICT, t["pk"].data_ptr(), t["sig"].data_ptr(),
+                          t["msg"].data_ptr(), nbm, o, l, n, v.data_ptr())
+            ks.dev_verify(0, st.cuda_stream, ntcrypto.NT_MODE_MIXED, t["k"].data_ptr(), t["sig"].data_ptr(),
+                          t["msg"].data_ptr(), nbm, o, l, n, kv.data_ptr())
+            be.dev_sha512(0, st.cuda_stream, t["msg"].data_ptr(), nbm, o, l, n, dg.data_ptr(), d_bad=cnt.data_ptr())
+            be.dev_sign(0, st.cuda_stream, t["seed"].data_ptr(), t["msg"].data_ptr(), nbm, o, l, n, spk.data_ptr(),
+                        ssig.data_ptr())
+        st.synchronize()
+        res[name] = dict(v=np.unpackbits(v.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool),
+                         kv=np.unpackbits(kv.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool),
+                         dg=dg.cpu().numpy(), cnt=int(cnt.item()), pk=spk.cpu().numpy(), sig=ssig.cpu().numpy())
+    ks.close()
+    g, b = res["good"], res["bad"]
+    assert g["v"].all() and g["kv"].all() and g["cnt"] == 0
+    for i in range(n):
+        o, l = int(off[i]), int(ln[i])
+        assert g["dg"][i].tobytes() == hashlib.sha512(msg[o:o + l].tobytes()).digest()[:32], i
+    assert np.array_equal(b["v"], ~bad) and np.array_equal(b["kv"], ~bad)
+    assert b["cnt"] == int(bad.sum())
+    assert not b["dg"][bad].any() and np.array_equal(b["dg"][~bad], g["dg"][~bad])
+    assert np.array_equal(b["pk"], g["pk"])
+    assert not b["sig"][bad].any() and np.array_equal(b["sig"][~bad], g["sig"][~bad])

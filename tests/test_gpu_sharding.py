@@ -6,6 +6,12 @@ import os
 import numpy as np
 import pytest
 
+
+def nbytes(t):
+    """byte size of a device tensor: the msg_bytes argument of the nt_dev_* entry points"""
+    return int(t.numel()) * int(t.element_size())
+
+
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 pytestmark = pytest.mark.gpu
 
@@ -217,9 +223,9 @@ def test_dev_api_batches_on_two_streams(pair):
     for i in range(24):
         k = i % 2
         s = streams[k].cuda_stream
-        one.dev_verify(0, s, ntcrypto.NT_MODE_STRICT, pk.data_ptr(), sig[k].data_ptr(), msg.data_ptr(),
+        one.dev_verify(0, s, ntcrypto.NT_MODE_STRICT, pk.data_ptr(), sig[k].data_ptr(), msg.data_ptr(), nbytes(msg),
                        off.data_ptr(), ln.data_ptr(), n, outs[k].data_ptr())
-        ks.dev_verify(0, s, ntcrypto.NT_MODE_STRICT, kidx.data_ptr(), sig[k].data_ptr(), msg.data_ptr(),
+        ks.dev_verify(0, s, ntcrypto.NT_MODE_STRICT, kidx.data_ptr(), sig[k].data_ptr(), msg.data_ptr(), nbytes(msg),
                       off.data_ptr(), ln.data_ptr(), n, kouts[k].data_ptr())
     torch.cuda.synchronize(dev)
     for k in range(2):

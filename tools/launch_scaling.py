@@ -8,6 +8,12 @@ import json
 import os
 import sys
 
+
+def nbytes(t):
+    """byte size of a device tensor: the msg_bytes argument of the nt_dev_* entry points"""
+    return int(t.numel()) * int(t.element_size())
+
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "narwhal-tusk_amd"))
 
@@ -29,13 +35,13 @@ def main():
     ln = torch.full((N,), L, dtype=torch.int64, device=dev)
     pk = torch.empty((N, 32), dtype=torch.uint8, device=dev)
     sig = torch.empty((N, 64), dtype=torch.uint8, device=dev)
-    be.dev_sign(0, sp, seeds.data_ptr(), msgs.data_ptr(), off.data_ptr(), ln.data_ptr(), N, pk.data_ptr(),
+    be.dev_sign(0, sp, seeds.data_ptr(), msgs.data_ptr(), nbytes(msgs), off.data_ptr(), ln.data_ptr(), N, pk.data_ptr(),
                 sig.data_ptr())
     out = torch.zeros(N // 64 + 1, dtype=torch.int64, device=dev)
     res = {}
     for n in (131072, 250000, 262144, 524288, 1048576):
         def step():
-            be.dev_verify(0, sp, ntcrypto.NT_MODE_STRICT, pk.data_ptr(), sig.data_ptr(), msgs.data_ptr(),
+            be.dev_verify(0, sp, ntcrypto.NT_MODE_STRICT, pk.data_ptr(), sig.data_ptr(), msgs.data_ptr(), nbytes(msgs),
                           off.data_ptr(), ln.data_ptr(), n, out.data_ptr())
         step()
         torch.cuda.synchronize()
@@ -54,7 +60,7 @@ def main():
             for c in range(4):
                 a = c * n
                 be.dev_verify(0, sp, ntcrypto.NT_MODE_STRICT, pk.data_ptr() + 32 * a, sig.data_ptr() + 64 * a,
-                              msgs.data_ptr(), off.data_ptr() + 8 * a, ln.data_ptr() + 8 * a, n,
+                              msgs.data_ptr(), nbytes(msgs), off.data_ptr() + 8 * a, ln.data_ptr() + 8 * a, n,
                               out.data_ptr() + 8 * (a // 64))
         chunked()
         torch.cuda.synchronize()
