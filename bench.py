@@ -157,22 +157,36 @@ def pipeline_streams(torch, be, dev, stream, n):
     return [stream] + [torch.cuda.Stream(dev) for _ in range(n - 1)]
 
 
-def fork_join(streams, stream):
-    """Events that bracket a pipelined region on `stream`: fork() makes every
-    pipeline stream wait for `stream`, join() makes `stream` wait for all of them."""
-    def fork(ev0):
-        for st in streams:
-            if st is not stream:
-                st.wait_event(ev0)
+class Region:
+    """A timed region whose steps run on several streams.  start(): an event on
+    `stream` that every other stream of the region waits for (complete when the
+    wait is issued: regions start after a barrier).  end(): an end event on
+    every stream; the region's GPU time is the latest of them.  There is no
+    GPU-side join: a wait for the other streams enqueued on an idle `stream`
+    stays pending for the whole region, and a cross-queue wait left pending
+    slowed the dispatches of the other hardware queues (short kernels ~5 us ->
+    ~50 us; config 3 on one library stream -5 %: profiles/r05/ab_join.txt)."""
 
-    def join():
-        import torch
-        for st in streams:
-            if st is not stream:
-                j = torch.cuda.Event()
-                j.record(st)
-                stream.wait_event(j)
-    return fork, join
+    def __init__(self, torch, streams, stream):
+        self.torch, self.stream = torch, stream
+        self.others = [s for s in streams if s.cuda_stream != stream.cuda_stream]
+
+    def start(self):
+        self.ev0 = self.torch.cuda.Event(enable_timing=True)
+        self.ev0.record(self.stream)
+        for st in self.others:
+            st.wait_event(self.ev0)
+
+    def end(self):
+        self.ends = []
+        for st in [self.stream] + self.others:
+            e = self.torch.cuda.Event(enable_timing=True)
+            e.record(st)
+            self.ends.append(e)
+
+    def ms(self):
+        """GPU time from start() to the last stream's end (call after a synchronize)"""
+        return max(self.ev0.elapsed_time(e) for e in self.ends)
 
 
 def side_streams(torch, dev, n):
@@ -325,7 +339,7 @@ def main():
     # (DESIGN.md §10), unlike config 3.
     nstreams = 2 if os.environ.get("NT_BENCH_STREAMS", "1") == "2" else 1
     streams = pipeline_streams(torch, be, dev, stream, nstreams)
-    fork, join = fork_join(streams, stream)
+    reg = Region(torch, streams, stream)
     outs = [torch.zeros(words, dtype=torch.int64, device=dev) for _ in range(2)]
     out = outs[0]
     lev = []  # per-launch (start, end) events: each launch's own duration (what rocprof reports)
@@ -344,18 +358,14 @@ def main():
     for i in range(args.warmup):
         step(i)
     barrier()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(stream)
-    fork(ev0)
+    reg.start()
     for i in range(args.steps):
         step(i, timed=True)
-    join()
-    ev1.record(stream)
+    reg.end()
     barrier()
     wall = time.perf_counter() - t0
-    step_ms = ev0.elapsed_time(ev1) / args.steps          # per batch, steady state
+    step_ms = reg.ms() / args.steps          # per batch, steady state
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in lev]))  # per launch
     ranks_cfg2 = nd.gather_object({"rank": rank, "device": local, "signatures": n, "kernel_ms": round(kernel_ms, 3),
                                    "gpu_ms_per_step": round(step_ms, 3),
@@ -551,7 +561,7 @@ def cfg2_two_streams(torch, be, dev, stream, ntcrypto, pk, sig, msgs, off, ln, n
     DESIGN.md §12).  The headline `value` unless NT_BENCH_HEADLINE=one; verdicts of both
     output buffers checked."""
     streams = pipeline_streams(torch, be, dev, stream, 2)
-    fork, join = fork_join(streams, stream)
+    reg = Region(torch, streams, stream)
     outs = [torch.zeros(words, dtype=torch.int64, device=dev) for _ in range(2)]
 
     def step(i):
@@ -562,15 +572,11 @@ def cfg2_two_streams(torch, be, dev, stream, ntcrypto, pk, sig, msgs, off, ln, n
     for i in range(max(2, args.warmup)):
         step(i)
     barrier()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(stream)
-    fork(ev0)
+    reg.start()
     for i in range(args.steps):
         step(i)
-    join()
-    ev1.record(stream)
+    reg.end()
     barrier()
     wall = max_over_ranks(time.perf_counter() - t0)
     mism = 0
@@ -578,7 +584,7 @@ def cfg2_two_streams(torch, be, dev, stream, ntcrypto, pk, sig, msgs, off, ln, n
         got = np.unpackbits(o.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
         mism += int((got != expect).sum())
     return {"verifies_per_s": round(n * world * args.steps / wall, 1), "ms_per_step": round(wall * 1e3 / args.steps, 3),
-            "gpu_ms_per_step": round(ev0.elapsed_time(ev1) / args.steps, 3),
+            "gpu_ms_per_step": round(reg.ms() / args.steps, 3),
             "mismatches_vs_expected": int(max_over_ranks(mism)),
             "note": "consecutive 1M batches alternating between two streams on different hardware queues; "
                     "the headline `value` is one stream, "
@@ -1000,20 +1006,16 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
         for i in range(max(1, args.warmup)):
             step(cached, i)
         barrier()
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        fork, join = fork_join(streams[:slots(cached)] + (side if side and slots(cached) > 1 else []), stream)
+        reg = Region(torch, streams[:slots(cached)] + (side if side and slots(cached) > 1 else []), stream)
         t0 = time.perf_counter()
-        ev0.record(stream)
-        fork(ev0)
+        reg.start()
         for i in range(steps):
             step(cached, i, timed=True)
-        join()
-        ev1.record(stream)
+        reg.end()
         barrier()
         wall_r = time.perf_counter() - t0
         wall = max_over_ranks(wall_r)
-        kms = ev0.elapsed_time(ev1) / steps
+        kms = reg.ms() / steps
         if key == "keyset":
             ranks3 = nd.gather_object({"rank": rank, "certificates": G, "signatures": G * (quorum + 1),
                                        "kernel_ms": round(kms, 3), "wall_ms_per_step": round(wall_r * 1e3 / steps, 3),
@@ -1040,23 +1042,35 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
         # candidate stream, interleaved twice, in one process
         saved = list(streams)
         lib = [torch.cuda.ExternalStream(be.dev_stream(0, k), device=dev) for k in range(2)]
-        cands = [("lib0", lib[0]), ("lib1", lib[1]), ("torch_cur", stream), ("torch_new", torch.cuda.Stream(dev))]
+        cands = [("lib0", lib[0]), ("torch_cur", stream)]
         ab = []
         mode_streams[True] = 1
+        # variants (profiles/r05/ab_join.txt): "region" = the timed regions above (per-stream end
+        # events); "gpujoin" = rounds 1-4's join (`stream` waits for the pipeline stream, a
+        # cross-queue wait enqueued on idle `stream` that stays pending for the region);
+        # "nokev" = region without the per-launch timing events
         for name, st in cands * 2:
-            streams[0] = st
-            barrier()
-            for i in range(2):
-                step(True, i)
-            barrier()
-            kev.clear()
-            t0 = time.perf_counter()
-            for i in range(20):
-                step(True, i, timed=True)
-            barrier()
-            wall = time.perf_counter() - t0
-            ab.append({"stream": name, "certs_per_s": round(G * 20 / wall, 1),
-                       "launch_ms": round(float(np.mean([a.elapsed_time(b) for a, b in kev])), 3)})
+            for var in ("region", "gpujoin", "nokev"):
+                streams[0] = st
+                barrier()
+                for i in range(max(1, args.warmup)):
+                    step(True, i)
+                barrier()
+                kev.clear()
+                reg = Region(torch, [st], stream)
+                t0 = time.perf_counter()
+                reg.start()
+                for i in range(20):
+                    step(True, i, timed=(var != "nokev"))
+                if var == "gpujoin" and st.cuda_stream != stream.cuda_stream:
+                    j = torch.cuda.Event()
+                    j.record(st)
+                    stream.wait_event(j)
+                reg.end()
+                barrier()
+                wall = time.perf_counter() - t0
+                ab.append({"stream": name, "variant": var, "certs_per_s": round(G * 20 / wall, 1),
+                           "launch_ms": round(float(np.mean([a.elapsed_time(b) for a, b in kev])), 3) if kev else None})
         streams[:] = saved
         mode_streams[True] = nst
         out["stream_ab"] = ab
@@ -1219,16 +1233,12 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream,
         for i in range(max(1, args.warmup)):
             step(i)
         barrier()
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        fork, join = fork_join(streams + (side or []), stream)
+        reg = Region(torch, streams + (side or []), stream)
         t0 = time.perf_counter()
-        ev0.record(stream)
-        fork(ev0)
+        reg.start()
         for i in range(steps):
             step(i, timed=True)
-        join()
-        ev1.record(stream)
+        reg.end()
         barrier()
         wall = time.perf_counter() - t0
         bad = 0
@@ -1242,7 +1252,7 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream,
         res[str(N)] = {"certificates": Gs, "signatures_per_launch": Vs + Gs, "steps": steps,
                        "certs_per_s": round(rate, 1),
                        "ms_per_step": round(wall * 1e3 / steps, 3),
-                       "gpu_ms_per_step": round(ev0.elapsed_time(ev1) / steps, 3),
+                       "gpu_ms_per_step": round(reg.ms() / steps, 3),
                        "keyset_launch_ms": round(float(np.mean([a.elapsed_time(b) for a, b in kev])), 3),
                        "per_gpu_vs_1gpu": round(rate / rate1, 3),
                        "expected_aggregate_certs_per_s": round(N * rate, 1), "mismatches_vs_expected": bad}

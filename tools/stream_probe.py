@@ -36,7 +36,8 @@ def main():
     pks = be.sign_batch(seeds_h)
     ks = be.keyset(pks)          # comb of B + key combs, built on library stream 0
     seeds = torch.from_numpy(seeds_h).to(dev)
-    cur = torch.cuda.current_stream()
+    cur = torch.cuda.Stream(dev)   # like bench.py: a created stream is torch's current one
+    torch.cuda.set_stream(cur)
     pre = torch.randint(0, 256, (G, 72), dtype=torch.uint8, device=dev)
     c_off = torch.arange(G, dtype=torch.int64, device=dev) * 72
     c_len = torch.full((G,), 72, dtype=torch.int64, device=dev)
@@ -79,9 +80,17 @@ def main():
         e[3].record(st)
         ev.append(e)
 
-    def run(phase):
+    def run(phase, fork=None, names=None):
         for name, st in streams().items():
+            if names and name not in names:
+                continue
             torch.cuda.synchronize()
+            if fork is not None:
+                # the bench's fork: this stream waits for an event recorded on torch's current stream
+                e0 = torch.cuda.Event(enable_timing=(fork == "timing"))
+                e0.record(cur)
+                if st.cuda_stream != cur.cuda_stream:
+                    st.wait_event(e0)
             evs = []
             t0 = time.perf_counter()
             for _ in range(reps):
@@ -95,12 +104,9 @@ def main():
                               "wall_ms_per_step": round(wall * 1e3, 3), "groups_ok": ok}), flush=True)
 
     run("after_setup")
-    # a large-scratch kernel (signing: ~936 B of spills per lane) on lib1 and torchA
-    for st in (streams()["lib1"], sA):
-        be.dev_sign(0, st.cuda_stream, sd.data_ptr(), cd.data_ptr(), nbytes(cd), m_off.data_ptr(), m_len.data_ptr(), 65536,
-                    tpk.data_ptr(), sig.data_ptr())
-    torch.cuda.synchronize()
-    run("after_sign_on_lib1_torchA")
+    for rnd in range(2):
+        for fk in ("timing", "plain", None):
+            run("fork_%s_%d" % (fk, rnd), fork=fk, names=("lib0", "torchA"))
     ks.close()
     be.close()
 
