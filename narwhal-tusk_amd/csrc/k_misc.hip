@@ -368,11 +368,12 @@ int keyset_occupancy() { return keyset_occ(); }
 hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
                          uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
                          const uint32_t* d_combB, int bbits, void* d_ws, uint32_t ws_slots, uint64_t* d_out_words,
-                         hipStream_t s) {
+                         hipStream_t s, int per_lane) {
   if (n == 0) return hipSuccess;
   if (!d_combB || !d_ws) return hipErrorInvalidValue;
-  const uint64_t blocks = verify_grid(n, ws_slots);
-#define NT_V_ARGS blocks, d_pk, d_sig, d_msg, msg_bytes, d_off, d_len, n, d_combB, d_ws, d_out_words, s
+  const int pl = verify_per_lane_for(per_lane);
+  const uint64_t blocks = verify_grid(n, ws_slots, pl);
+#define NT_V_ARGS blocks, d_pk, d_sig, d_msg, msg_bytes, d_off, d_len, n, d_combB, d_ws, d_out_words, s, pl
   if (bbits == kBCombBits)
     return mode == kStrict ? launch_verify_m<kStrict, kBCombBits>(NT_V_ARGS)
                            : launch_verify_m<kCofactorless, kBCombBits>(NT_V_ARGS);
@@ -686,8 +687,10 @@ size_t wcomb_fill_tmp_bytes_per_key(int bits) { return comb_size(bits, 2); }
 // keys per fill launch: >= 128k threads per launch (16 keys at W = 16, 2 at W = 20)
 uint32_t wcomb_fill_batch(int bits) { return (uint32_t)comb_size(bits, 3); }
 // verify grid: one 512-signature block per workspace slot, at most ws_slots
-uint64_t verify_grid(uint64_t n, uint32_t ws_slots) {
-  const uint64_t blocks = (n + kVPer * kBlock - 1) / (kVPer * kBlock);  // kVPer signatures per lane
+int verify_per_lane_for(int per_lane) { return per_lane == 1 && verify_occupancy() == 2 ? 1 : kVPer; }
+uint64_t verify_grid(uint64_t n, uint32_t ws_slots, int per_lane) {
+  const uint64_t per = (uint64_t)verify_per_lane_for(per_lane) * kBlock;  // signatures per block iteration
+  const uint64_t blocks = (n + per - 1) / per;
   return blocks < ws_slots ? blocks : ws_slots;
 }
 
@@ -698,7 +701,9 @@ uint64_t verify_grid(uint64_t n, uint32_t ws_slots) {
 uint64_t keyset_round_sigs(uint32_t cus) {
   return (uint64_t)cus * 4 * keyset_occ() * 64 * std::min<uint32_t>(keyset_per_lane(), 8);
 }
-uint64_t verify_round_sigs(uint32_t cus) { return (uint64_t)cus * verify_occupancy() * kVPer * kBlock; }
+uint64_t verify_round_sigs(uint32_t cus, int per_lane) {
+  return (uint64_t)cus * verify_occupancy() * verify_per_lane_for(per_lane) * kBlock;
+}
 // most rows (signatures per lane) of a key-cache chunk, one inversion each: 64,
 // the plan picks the chunk size (ks_plan.hpp; round-3 A/B in DESIGN.md §5.2);
 // NT_KEYSET_PER_LANE in [1, kKsPerLane] caps it for A/B runs

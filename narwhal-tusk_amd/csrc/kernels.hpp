@@ -21,7 +21,7 @@ hipError_t launch_sha512_trunc32(const uint8_t* d_data, uint64_t data_bytes, con
 hipError_t launch_verify(int mode, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
                          uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
                          const uint32_t* d_combB, int bbits, void* d_ws, uint32_t ws_slots, uint64_t* d_out_words,
-                         hipStream_t s);
+                         hipStream_t s, int per_lane = 0);
 hipError_t launch_group_and(const uint64_t* d_first, const uint32_t* d_cnt, uint64_t G,
                             const uint64_t* d_sig_words, uint64_t* d_group_words, hipStream_t s);
 // off[first[g] + q] = 32 g, len = 32 for q < cnt[g] (groups' 32-byte messages)
@@ -47,8 +47,11 @@ size_t keyset_sort_bytes(uint64_t n);
 KsPlan keyset_plan(uint64_t n, uint32_t cus);
 // signatures one full round of the launch covers (host-side chunk sizing)
 uint64_t keyset_round_sigs(uint32_t cus);
-uint64_t verify_grid(uint64_t n, uint32_t ws_slots);  // blocks of a launch_verify
-uint64_t verify_round_sigs(uint32_t cus);
+// signatures per lane of a launch_verify: per_lane 0 = the build's default (kVPer, 2);
+// 1 = one per lane (half the launch latency; host entry points' short chunks)
+int verify_per_lane_for(int per_lane);
+uint64_t verify_grid(uint64_t n, uint32_t ws_slots, int per_lane = 0);  // blocks of a launch_verify
+uint64_t verify_round_sigs(uint32_t cus, int per_lane = 0);
 uint32_t keyset_per_lane();
 // per-wave stash of a launch over n signatures (d_stash above)
 size_t keyset_stash_bytes(uint64_t n, uint32_t cus);

@@ -224,7 +224,7 @@ struct KsStash {
 template <int MODE, int WB>
 hipError_t launch_verify_m(uint64_t blocks, const uint8_t* d_pk, const uint8_t* d_sig, const uint8_t* d_msg,
                            uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
-                           const uint32_t* d_combB, void* d_ws, uint64_t* d_out_words, hipStream_t s);
+                           const uint32_t* d_combB, void* d_ws, uint64_t* d_out_words, hipStream_t s, int per_lane);
 template <int MODE, int WA, int WB>
 hipError_t launch_keyset_m(const KsPlan& plan, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                            uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,

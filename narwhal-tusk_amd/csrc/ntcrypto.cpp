@@ -460,22 +460,27 @@ int msg_prepare(Device& dv, const uint64_t* off, const uint64_t* len, uint64_t l
   ms.whole = sum > ms.span + ms.span / 4 + 4096;
   const uint64_t m = ch.back().second;
   NT_CHK(dv.d[B_DATA].ensure(ms.span + 64));
-  NT_CHK(dv.d[B_OFF].ensure(std::max<uint64_t>(m, 1) * 8));
-  NT_CHK(dv.d[B_LEN].ensure(std::max<uint64_t>(m, 1) * 8));
-  NT_CHK(dv.h[B_OFF].ensure(std::max<uint64_t>(m, 1) * 8));
-  NT_CHK(dv.h[B_LEN].ensure(std::max<uint64_t>(m, 1) * 8));
+  NT_CHK(dv.d[B_OFF].ensure(std::max<uint64_t>(m, 1) * 16));
+  NT_CHK(dv.h[B_OFF].ensure(std::max<uint64_t>(m, 1) * 16));
   return NT_OK;
+}
+
+// Device offsets / lengths of chunk [a, b) staged by msg_copy: words [2a, 2b) of
+// B_OFF hold the chunk's b - a rebased offsets, then its b - a lengths (one copy)
+inline const uint64_t* chunk_off(Device& dv, uint64_t a) { return dv.d[B_OFF].as<uint64_t>() + 2 * a; }
+inline const uint64_t* chunk_len(Device& dv, uint64_t a, uint64_t b) {
+  return dv.d[B_OFF].as<uint64_t>() + 2 * a + (b - a);
 }
 
 // copies (copy stream) of chunk c = items [lo + a, lo + b): rebased offsets,
 // lengths, and the chunk's message bytes
 int msg_copy(Device& dv, const uint8_t* data, const uint64_t* off, const uint64_t* len, uint64_t lo,
              const MsgStage& ms, size_t c, uint64_t a, uint64_t b) {
-  uint64_t* ho = dv.h[B_OFF].as<uint64_t>();
-  uint64_t* hl = dv.h[B_LEN].as<uint64_t>();
+  uint64_t* ho = dv.h[B_OFF].as<uint64_t>() + 2 * a;
+  uint64_t* hl = ho + (b - a);
   for (uint64_t i = a; i < b; ++i) {
-    ho[i] = len[lo + i] ? off[lo + i] - ms.base : 0;
-    hl[i] = len[lo + i];
+    ho[i - a] = len[lo + i] ? off[lo + i] - ms.base : 0;
+    hl[i - a] = len[lo + i];
   }
   const auto& pc = ms.piece[c];
   if (ms.whole) {
@@ -485,11 +490,100 @@ int msg_copy(Device& dv, const uint8_t* data, const uint64_t* off, const uint64_
     NT_TRY(hipMemcpyAsync(dv.d[B_DATA].as<uint8_t>() + (pc.first - ms.base), data + pc.first, pc.second - pc.first,
                           hipMemcpyHostToDevice, dv.cstream));
   }
-  if (b > a) {
-    NT_TRY(hipMemcpyAsync(dv.d[B_OFF].as<uint64_t>() + a, ho + a, (b - a) * 8, hipMemcpyHostToDevice, dv.cstream));
-    NT_TRY(hipMemcpyAsync(dv.d[B_LEN].as<uint64_t>() + a, hl + a, (b - a) * 8, hipMemcpyHostToDevice, dv.cstream));
+  if (b > a)
+    NT_TRY(hipMemcpyAsync(dv.d[B_OFF].as<uint64_t>() + 2 * a, ho, (b - a) * 16, hipMemcpyHostToDevice, dv.cstream));
+  return NT_OK;
+}
+
+// every message byte a staged call copies lies in nt_host_alloc memory
+bool ms_pinned(const MsgStage& ms, const uint8_t* data) {
+  if (ms.span == 0) return true;
+  if (ms.whole) return is_pinned(data + ms.base, ms.span);
+  for (const auto& pc : ms.piece)
+    if (pc.second > pc.first && !is_pinned(data + pc.first, pc.second - pc.first)) return false;
+  return true;
+}
+
+// The chunk pipeline of a host entry point: copies(c) on the copy stream, then
+// kernels(c) on compute stream cstr(c), launched by the host once it has waited
+// for chunk c's copies -- a compute stream never holds a wait for the copy
+// stream (a cross-queue wait pending at the head of a hardware queue slows the
+// dispatches of the other queues: profiles/r05/ab_join.txt).  With every source
+// in pinned memory (`async`) hipMemcpyAsync returns at once, and the copies of
+// chunk c + 1 are queued before the host waits for chunk c, so the link never
+// idles.  From pageable memory HIP stages the copy and returns when it is done
+// (NT_PIPE_TRACE, profiles/r05/host_pipe_*.txt): then chunk c's kernels are
+// launched before the copies of chunk c + 1 are issued, so they run under them.
+// Returns with every kernel launched; finish_chunks() then waits for both
+// compute streams on the host.
+// NT_PIPE_TRACE=1: host timestamps of every step of run_chunks on stderr (diagnosis)
+static bool pipe_trace() {
+  static const bool on = [] {
+    const char* e = std::getenv("NT_PIPE_TRACE");
+    return e && *e == '1';
+  }();
+  return on;
+}
+static double pipe_now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+template <class Copy, class Launch>
+int run_chunks(Device& dv, size_t C, bool async, Copy&& copy, Launch&& launch) {
+  if (C == 0) return NT_OK;
+  if (C > (size_t)kMaxChunks) return NT_EINVAL;
+  const bool tr = pipe_trace();
+  const double t0 = tr ? pipe_now_us() : 0.0;
+  auto issue = [&](size_t c) -> int {
+    NT_CHK(copy(c));
+    NT_TRY(hipEventRecord(dv.cev[c], dv.cstream));
+    if (tr) std::fprintf(stderr, "[pipe] %9.1f copies %zu issued%s\n", pipe_now_us() - t0, c, async ? "" : " (staged)");
+    return NT_OK;
+  };
+  if (async) NT_CHK(issue(0));
+  for (size_t c = 0; c < C; ++c) {
+    if (!async) NT_CHK(issue(c));
+    else if (c + 1 < C) NT_CHK(issue(c + 1));
+    NT_TRY(hipEventSynchronize(dv.cev[c]));
+    if (tr) std::fprintf(stderr, "[pipe] %9.1f copies %zu done\n", pipe_now_us() - t0, c);
+    NT_CHK(launch(c));
+    if (tr) std::fprintf(stderr, "[pipe] %9.1f kernels %zu launched\n", pipe_now_us() - t0, c);
   }
   return NT_OK;
+}
+
+// both compute streams drained (host-side), so work issued next on dv.stream
+// follows every chunk's kernels without a cross-queue wait
+int finish_chunks(Device& dv) {
+  if (dv.stream2 != dv.stream) NT_TRY(hipStreamSynchronize(dv.stream2));
+  return NT_OK;
+}
+
+// Chunks of a host verify call (one round R1 = the signatures one wave of
+// resident waves covers at ONE signature per lane).  The call is PCIe-bound --
+// 608 B per verify over ~50 GB/s against ~95 verifies per us of kernel -- and
+// its copies run back to back, so it ends one kernel latency after the last
+// copy; a launch's latency is its lanes' serial signatures.  So: a quarter
+// round first (the first kernel starts after a short copy), whole rounds at
+// one signature per lane in the middle (a round's copy ~ its kernel), and a
+// last chunk of at most half a round (one wave per SIMD: the shortest tail).
+// More than kMaxChunks - 2 middle chunks grow by whole rounds.
+std::vector<uint64_t> verify_chunk_targets(uint64_t total, uint64_t R1) {
+  const uint64_t cap = (uint64_t)pipe_chunks_cap();
+  const uint64_t half = std::max<uint64_t>(64, R1 / 2 / 64 * 64), quarter = std::max<uint64_t>(64, R1 / 4 / 64 * 64);
+  if (cap < 3 || total <= half + quarter) return {total};
+  std::vector<uint64_t> t{quarter};
+  // the last chunk starts on a multiple of 64 (every chunk owns whole verdict words)
+  const uint64_t last_start = std::max(quarter, (total - half + 63) / 64 * 64);
+  uint64_t mid = last_start - quarter;
+  const uint64_t per = std::max<uint64_t>(R1, ((mid + cap - 3) / (cap - 2) + R1 - 1) / R1 * R1);
+  while (mid > 0) {
+    const uint64_t c = std::min(per, mid);
+    t.push_back(c);
+    mid -= c;
+  }
+  t.push_back(total - last_start);
+  return t;
 }
 
 // Item counts per chunk.  A host call is PCIe-bound (config 2: 608 B per
@@ -682,17 +776,18 @@ int nt_sha512_trunc32(nt_ctx* ctx, const uint8_t* data, const uint64_t* off, con
     MsgStage ms;
     NT_CHK(msg_prepare(dv, off, len, lo, ch, ms));
     NT_CHK(dv.d[B_OUT].ensure(m * 32));
-    for (size_t c = 0; c < ch.size(); ++c) {
+    NT_CHK(run_chunks(dv, ch.size(), ms_pinned(ms, data), [&](size_t c) -> int {
+      return msg_copy(dv, data, off, len, lo, ms, c, ch[c].first, ch[c].second);
+    }, [&](size_t c) -> int {
       const uint64_t a = ch[c].first, b = ch[c].second;
-      NT_CHK(msg_copy(dv, data, off, len, lo, ms, c, a, b));
-      NT_TRY(dv.fence((int)c));
       uint64_t ml = 0;  // the chunk's longest message selects the kernel
       for (uint64_t i = lo + a; i < lo + b; ++i) ml = std::max(ml, len[i]);
-      NT_TRY(nt::launch_sha512_trunc32(dv.d[B_DATA].as<uint8_t>(), ms.span, dv.d[B_OFF].as<uint64_t>() + a,
-                                       dv.d[B_LEN].as<uint64_t>() + a, b - a, dv.d[B_OUT].as<uint8_t>() + 32 * a,
+      NT_TRY(nt::launch_sha512_trunc32(dv.d[B_DATA].as<uint8_t>(), ms.span, chunk_off(dv, a),
+                                       chunk_len(dv, a, b), b - a, dv.d[B_OUT].as<uint8_t>() + 32 * a,
                                        dv.cstr((int)c), ml));
-    }
-    NT_TRY(dv.join());
+      return NT_OK;
+    }));
+    NT_CHK(finish_chunks(dv));
     NT_TRY(hipMemcpyAsync(out32 + 32 * lo, dv.d[B_OUT].p, m * 32, hipMemcpyDeviceToHost, dv.stream));
     NT_TRY(hipStreamSynchronize(dv.stream));
     return NT_OK;
@@ -717,27 +812,39 @@ int nt_ed25519_verify_strict(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* si
   return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
     NT_CHK(verify_tables(dv));
     const uint64_t m = hi - lo, words = (m + 63) / 64;
-    const auto ch = plan_chunks(m, pipe_round(nt::verify_round_sigs(dv.cus)));
+    const uint64_t R1 = pipe_round(nt::verify_round_sigs(dv.cus, 1));
+    std::vector<std::pair<uint64_t, uint64_t>> ch;
+    {
+      uint64_t a = 0;
+      for (uint64_t t : verify_chunk_targets(m, R1)) {
+        ch.emplace_back(a, a + t);
+        a += t;
+      }
+    }
     MsgStage ms;
     NT_CHK(msg_prepare(dv, off, len, lo, ch, ms));
     NT_CHK(dv.d[B_PK].ensure(m * 32));
     NT_CHK(dv.d[B_SIG].ensure(m * 64));
     NT_CHK(dv.d[B_OUT].ensure(words * 8));
     NT_CHK(dv.h[B_OUT].ensure(words * 8));
-    for (size_t c = 0; c < ch.size(); ++c) {
+    const bool pinned = ms_pinned(ms, msg) && is_pinned(pk32 + 32 * lo, 32 * m) && is_pinned(sig64 + 64 * lo, 64 * m);
+    NT_CHK(run_chunks(dv, ch.size(), pinned, [&](size_t c) -> int {
       const uint64_t a = ch[c].first, b = ch[c].second;
       NT_CHK(msg_copy(dv, msg, off, len, lo, ms, c, a, b));
       NT_TRY(hipMemcpyAsync(dv.d[B_PK].as<uint8_t>() + 32 * a, pk32 + 32 * (lo + a), (b - a) * 32,
                             hipMemcpyHostToDevice, dv.cstream));
       NT_TRY(hipMemcpyAsync(dv.d[B_SIG].as<uint8_t>() + 64 * a, sig64 + 64 * (lo + a), (b - a) * 64,
                             hipMemcpyHostToDevice, dv.cstream));
-      NT_TRY(dv.fence((int)c));
-      NT_CHK(dv.verify_chunk((int)c, NT_MODE_STRICT, dv.d[B_PK].as<uint8_t>() + 32 * a,
+      return NT_OK;
+    }, [&](size_t c) -> int {
+      const uint64_t a = ch[c].first, b = ch[c].second;
+      // chunks of at most one round: one signature per lane (half the launch latency)
+      return dv.verify_chunk((int)c, NT_MODE_STRICT, dv.d[B_PK].as<uint8_t>() + 32 * a,
                              dv.d[B_SIG].as<uint8_t>() + 64 * a, dv.d[B_DATA].as<uint8_t>(), ms.span,
-                             dv.d[B_OFF].as<uint64_t>() + a, dv.d[B_LEN].as<uint64_t>() + a, b - a,
-                             dv.d[B_OUT].as<uint64_t>() + a / 64));
-    }
-    NT_TRY(dv.join());
+                             chunk_off(dv, a), chunk_len(dv, a, b), b - a, dv.d[B_OUT].as<uint64_t>() + a / 64,
+                             b - a <= R1 ? 1 : 0);
+    }));
+    NT_CHK(finish_chunks(dv));
     NT_TRY(hipMemcpyAsync(dv.h[B_OUT].p, dv.d[B_OUT].p, words * 8, hipMemcpyDeviceToHost, dv.stream));
     NT_TRY(hipStreamSynchronize(dv.stream));
     words_to_bitmap(out_bitmap + lo / 8, dv.h[B_OUT].as<uint64_t>(), m);
@@ -853,8 +960,9 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
     uint64_t* hfirst = dv.h[B_FIRST].as<uint64_t>();
     uint32_t* hcnt = dv.h[B_CNT].as<uint32_t>();
     hipStream_t cs = dv.cstream;
-    NT_TRY(hipMemsetAsync(dv.d[B_OUT].p, 0, sw * 8 + 8, cs));  // before every fence
-    for (size_t c = 0; c < C; ++c) {
+    NT_TRY(hipMemsetAsync(dv.d[B_OUT].p, 0, sw * 8 + 8, cs));  // before chunk 0's copy-done event
+    // staged groups are in the library's pinned staging; direct ones in the caller's
+    NT_CHK(run_chunks(dv, C, is_pinned(msg32 + 32 * glo, 32 * gm), [&](size_t c) -> int {
       const uint64_t g0 = ch[c].first, g1 = ch[c].second, gl = g0 - glo, e0 = E[c], mc = E[c + 1] - E[c];
       // chunk-local: hfirst relative to e0; message offsets 32 * (g - g0) made on the device
       stage_groups(g0, g1, first, cnt, kw, keys, sig64, hkey + kw * e0, hsig + 64 * e0, hfirst + gl, hcnt + gl,
@@ -869,7 +977,9 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
                             hipMemcpyHostToDevice, cs));
       NT_TRY(hipMemcpyAsync(dv.d[B_FIRST].as<uint64_t>() + gl, hfirst + gl, (g1 - g0) * 8, hipMemcpyHostToDevice, cs));
       NT_TRY(hipMemcpyAsync(dv.d[B_CNT].as<uint32_t>() + gl, hcnt + gl, (g1 - g0) * 4, hipMemcpyHostToDevice, cs));
-      NT_TRY(dv.fence((int)c));
+      return NT_OK;
+    }, [&](size_t c) -> int {
+      const uint64_t g0 = ch[c].first, g1 = ch[c].second, gl = g0 - glo, e0 = E[c], mc = E[c + 1] - E[c];
       hipStream_t s = dv.cstr((int)c);
       const uint8_t* dk = dv.d[B_PK].as<uint8_t>() + kw * e0;
       const uint8_t* dsig = dv.d[B_SIG].as<uint8_t>() + 64 * e0;
@@ -895,9 +1005,10 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
       }
       NT_TRY(nt::launch_group_and(dv.d[B_FIRST].as<uint64_t>() + gl, dv.d[B_CNT].as<uint32_t>() + gl, g1 - g0, dout,
                                   dv.d[B_OUT2].as<uint64_t>() + gl / 64, s));
-    }
+      return NT_OK;
+    }));
     hipStream_t s = dv.stream;
-    NT_TRY(dv.join());
+    NT_CHK(finish_chunks(dv));
     NT_TRY(hipMemcpyAsync(dv.h[B_OUT2].p, dv.d[B_OUT2].p, gw * 8, hipMemcpyDeviceToHost, s));
     if (out_sig_bitmap && m)
       NT_TRY(hipMemcpyAsync(dv.h[B_OUT].p, dv.d[B_OUT].p, sw * 8, hipMemcpyDeviceToHost, s));
@@ -1133,26 +1244,29 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
     for (const auto& c : ch) mc = std::max(mc, c.second - c.first);
     NT_CHK(dv.ensure_stash(0, mc));
     if (ch.size() > 1) NT_CHK(dv.ensure_stash(1, mc));
-    for (size_t c = 0; c < ch.size(); ++c) {
+    const bool pinned = ms_pinned(ms, msg) && is_pinned(key_idx + lo, 4 * m) && is_pinned(sig64 + 64 * lo, 64 * m);
+    NT_CHK(run_chunks(dv, ch.size(), pinned, [&](size_t c) -> int {
       const uint64_t a = ch[c].first, b = ch[c].second;
       NT_CHK(msg_copy(dv, msg, off, len, lo, ms, c, a, b));
       NT_TRY(hipMemcpyAsync(dv.d[B_PK].as<uint32_t>() + a, key_idx + lo + a, (b - a) * 4, hipMemcpyHostToDevice,
                             dv.cstream));
       NT_TRY(hipMemcpyAsync(dv.d[B_SIG].as<uint8_t>() + 64 * a, sig64 + 64 * (lo + a), (b - a) * 64,
                             hipMemcpyHostToDevice, dv.cstream));
-      NT_TRY(dv.fence((int)c));
+      return NT_OK;
+    }, [&](size_t c) -> int {
+      const uint64_t a = ch[c].first, b = ch[c].second;
       void* st = (c & 1) ? dv.stash2.p : dv.d[B_STASH].p;
       void* so = (c & 1) ? dv.sort2.p : dv.d[B_SORT].p;
       hipStream_t s = dv.cstr((int)c);
-      NT_CHK(dv.keyset_launch(s, st, [&] {
+      return dv.keyset_launch(s, st, [&] {
         return nt::launch_verify_keyset(mode, ks->bits, dv.d[B_PK].as<uint32_t>() + a,
                                         dv.d[B_SIG].as<uint8_t>() + 64 * a, dv.d[B_DATA].as<uint8_t>(), ms.span,
-                                        dv.d[B_OFF].as<uint64_t>() + a, dv.d[B_LEN].as<uint64_t>() + a, b - a,
+                                        chunk_off(dv, a), chunk_len(dv, a, b), b - a,
                                         pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, dv.bbits, st, so,
                                         dv.d[B_OUT].as<uint64_t>() + a / 64, dv.cus, s);
-      }));
-    }
-    NT_TRY(dv.join());
+      });
+    }));
+    NT_CHK(finish_chunks(dv));
     NT_TRY(hipMemcpyAsync(dv.h[B_OUT].p, dv.d[B_OUT].p, words * 8, hipMemcpyDeviceToHost, dv.stream));
     NT_TRY(hipStreamSynchronize(dv.stream));
     words_to_bitmap(out_bitmap + lo / 8, dv.h[B_OUT].as<uint64_t>(), m);

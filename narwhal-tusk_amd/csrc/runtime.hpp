@@ -172,15 +172,16 @@ struct Device {
   uint32_t cus = 0;
   hipEvent_t ws_done = nullptr;  // orders every kernel that uses d_ws, whatever its stream
   hipEvent_t stash_done = nullptr;  // same for the key-cache stash d[B_STASH] (host and device API)
-  // host entry points: chunk c's H2D copies go on cstream and chunk c's kernels
-  // wait for cev[c] on `stream`, so copies of chunk c+1 overlap kernels of chunk c
+  // host entry points: chunk c's H2D copies go on cstream, cev[c] marks them
+  // done, and the host launches chunk c's kernels once it has waited for cev[c]
+  // (ntcrypto.cpp run_chunks), so copies of chunk c+1 overlap kernels of chunk c
   hipStream_t cstream = nullptr;
   hipEvent_t cev[16] = {};
   // ... and chunks alternate between two compute streams, so the waves of chunk
   // c+1 fill the CUs that chunk c's last waves leave idle.  Stream 2 has its own
   // verify workspace and key-cache stash.
   hipStream_t stream2 = nullptr;
-  hipEvent_t join2 = nullptr, ws2_done = nullptr, stash2_done = nullptr;
+  hipEvent_t ws2_done = nullptr, stash2_done = nullptr;
   DevBuf ws2, stash2, sort2;
   std::mutex mu;
   uint64_t dev_calls = 0;  // device-API verify calls (workspace alternation), under mu
@@ -217,7 +218,6 @@ struct Device {
     if (ws2.p) (void)hipFree(ws2.p);
     if (stash2.p) (void)hipFree(stash2.p);
     if (sort2.p) (void)hipFree(sort2.p);
-    if (join2) (void)hipEventDestroy(join2);
     if (ws2_done) (void)hipEventDestroy(ws2_done);
     if (stash2_done) (void)hipEventDestroy(stash2_done);
     if (stream2 && stream2 != stream) (void)hipStreamDestroy(stream2);
@@ -253,7 +253,6 @@ struct Device {
     NT_TRY(hipEventCreateWithFlags(&ws_done, hipEventDisableTiming));
     NT_TRY(hipEventCreateWithFlags(&stash_done, hipEventDisableTiming));
     for (auto& e : cev) NT_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    NT_TRY(hipEventCreateWithFlags(&join2, hipEventDisableTiming));
     NT_TRY(hipEventCreateWithFlags(&ws2_done, hipEventDisableTiming));
     NT_TRY(hipEventCreateWithFlags(&stash2_done, hipEventDisableTiming));
     // Nothing large is allocated here: the comb of B and the verify workspace
@@ -314,32 +313,19 @@ struct Device {
   // compute stream of chunk c
   hipStream_t cstr(int c) const { return (c & 1) ? stream2 : stream; }
 
-  // the kernels of chunk c wait for the copies issued so far on cstream
-  hipError_t fence(int c) {
-    hipError_t e = hipEventRecord(cev[c], cstream);
-    if (e != hipSuccess) return e;
-    return hipStreamWaitEvent(cstr(c), cev[c], 0);
-  }
-
-  // `stream` waits for everything issued on stream2
-  hipError_t join() {
-    hipError_t e = hipEventRecord(join2, stream2);
-    if (e != hipSuccess) return e;
-    return hipStreamWaitEvent(stream, join2, 0);
-  }
-
   // verify launch of chunk c: even chunks use the device workspace on `stream`,
-  // odd chunks stream2's own workspace (grown to the chunk's grid)
+  // odd chunks stream2's own workspace (grown to the chunk's grid); per_lane as
+  // in nt::launch_verify
   int verify_chunk(int c, int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint64_t msg_bytes,
-                   const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out) {
+                   const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out, int per_lane = 0) {
     if (!(c & 1))
-      return verify(mode, pk, sig, msg, msg_bytes, off, len, n, out, stream) == hipSuccess ? NT_OK : NT_EHIP;
-    const uint64_t blocks = nt::verify_grid(n, ws_slots);
+      return verify(mode, pk, sig, msg, msg_bytes, off, len, n, out, stream, per_lane) == hipSuccess ? NT_OK : NT_EHIP;
+    const uint64_t blocks = nt::verify_grid(n, ws_slots, per_lane);
     const int rc = grow_ws2(blocks);
     if (rc != NT_OK) return rc;
     if (hipStreamWaitEvent(stream2, ws2_done, 0) != hipSuccess ||
         nt::launch_verify(mode, pk, sig, msg, msg_bytes, off, len, n, d_combB, bbits, ws2.p,
-                          (uint32_t)std::max<uint64_t>(blocks, 1), out, stream2) != hipSuccess ||
+                          (uint32_t)std::max<uint64_t>(blocks, 1), out, stream2, per_lane) != hipSuccess ||
         hipEventRecord(ws2_done, stream2) != hipSuccess)
       return NT_EHIP;
     return NT_OK;
@@ -403,10 +389,12 @@ struct Device {
 
   // verify launch that shares the workspace: wait for the previous user, then mark
   hipError_t verify(int mode, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg, uint64_t msg_bytes,
-                    const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out, hipStream_t s) {
+                    const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* out, hipStream_t s,
+                    int per_lane = 0) {
     hipError_t e = hipStreamWaitEvent(s, ws_done, 0);
     if (e != hipSuccess) return e;
-    e = nt::launch_verify(mode, pk, sig, msg, msg_bytes, off, len, n, d_combB, bbits, d_ws, ws_slots, out, s);
+    e = nt::launch_verify(mode, pk, sig, msg, msg_bytes, off, len, n, d_combB, bbits, d_ws, ws_slots, out, s,
+                          per_lane);
     if (e != hipSuccess) return e;
     return hipEventRecord(ws_done, s);
   }

@@ -40,6 +40,7 @@ def main():
         be.verify_strict(args[0], args[1], args[2], off, ln)
         ts = []
         for _ in range(a.reps):
+            print("[probe] %s call" % name, file=sys.stderr, flush=True)
             t0 = time.perf_counter()
             r = be.verify_strict(args[0], args[1], args[2], off, ln)
             ts.append(time.perf_counter() - t0)
