@@ -205,6 +205,9 @@ def side_streams(torch, dev, n):
 
 
 _T0 = time.time()
+# NT_BENCH_SIDE_JOIN=0 (A/B): the pipeline stream does not wait for its step's
+# side-stream header-id digests (the region's end events and barrier still do)
+SIDE_JOIN = os.environ.get("NT_BENCH_SIDE_JOIN", "1") != "0"
 
 
 def progress(what):
@@ -964,7 +967,8 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
             if timed:
                 kev[-1][1].record(st)
             if side and slots(cached) > 1:
-                st.wait_event(hev)
+                if SIDE_JOIN:
+                    st.wait_event(hev)
             else:
                 be.dev_sha512(0, sq, hdr_flat.data_ptr(), nbytes(hdr_flat), h_off.data_ptr(), h_len.data_ptr(), G, b["hd2"].data_ptr(),
                               max_len=hlen)
@@ -1223,7 +1227,8 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream,
             if timed:
                 kev[-1][1].record(st)
             if side:
-                st.wait_event(hev)
+                if SIDE_JOIN:
+                    st.wait_event(hev)
             else:
                 be.dev_sha512(0, sq, t["hdr_flat"].data_ptr(), nbytes(t["hdr_flat"]), t["h_off"].data_ptr(), t["h_len"].data_ptr(), Gs,
                               b["hd2"].data_ptr(), max_len=t["hlen"])

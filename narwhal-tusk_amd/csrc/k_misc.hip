@@ -687,7 +687,12 @@ size_t wcomb_fill_tmp_bytes_per_key(int bits) { return comb_size(bits, 2); }
 // keys per fill launch: >= 128k threads per launch (16 keys at W = 16, 2 at W = 20)
 uint32_t wcomb_fill_batch(int bits) { return (uint32_t)comb_size(bits, 3); }
 // verify grid: one 512-signature block per workspace slot, at most ws_slots
-int verify_per_lane_for(int per_lane) { return per_lane == 1 && verify_occupancy() == 2 ? 1 : kVPer; }
+int verify_per_lane_for(int per_lane) {
+  // NT_VERIFY_NPER=1 (A/B): one signature per lane for every launch that does not ask
+  static const int dflt = env_occ("NT_VERIFY_NPER", kVPer, 1, 2);
+  const int p = per_lane ? per_lane : dflt;
+  return p == 1 && verify_occupancy() == 2 ? 1 : kVPer;
+}
 uint64_t verify_grid(uint64_t n, uint32_t ws_slots, int per_lane) {
   const uint64_t per = (uint64_t)verify_per_lane_for(per_lane) * kBlock;  // signatures per block iteration
   const uint64_t blocks = (n + per - 1) / per;

@@ -48,6 +48,9 @@ constexpr int kAQuads = NT_ATAB_SIGNED ? 15 : 10;  // uint4 per entry
 // --------------------------------------------------------------------------
 // Wide comb of one point with digit width W, layout [pos][entry][32 words];
 // 8 x 16-byte loads.
+#ifndef NT_COMB_NT
+#define NT_COMB_NT 0
+#endif
 template <int W>
 struct WideComb {
   static constexpr int kBits = W;
@@ -60,7 +63,14 @@ struct WideComb {
     uint32_t w[32];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+#if NT_COMB_NT
+      // A/B build (-DNT_COMB_NT=1): non-temporal loads -- a random comb line is read once
+      typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+      const u4v t = __builtin_nontemporal_load((const u4v*)e + i);
+      const uint4 v = make_uint4(t.x, t.y, t.z, t.w);
+#else
       const uint4 v = e[i];
+#endif
       w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
     }
 #pragma unroll

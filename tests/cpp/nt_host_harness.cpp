@@ -14,6 +14,7 @@
 #include "../../narwhal-tusk_amd/csrc/ed25519_ops.hpp"
 #include "../../narwhal-tusk_amd/csrc/fe_inv_vt.hpp"
 #include "../../narwhal-tusk_amd/csrc/ks_plan.hpp"
+#include "../../narwhal-tusk_amd/csrc/pipe_plan.hpp"
 
 namespace nt {
 unsigned long long g_fe_mul = 0, g_fe_sq = 0;
@@ -407,6 +408,27 @@ void nth_ks_plan(unsigned long long n, uint32_t cus, uint32_t cap, int force, ui
 // the stash bound every plan of a launch of <= rows rows fits in (ks_plan.hpp)
 unsigned long long nth_ks_stash_rows_bound(unsigned long long rows, uint32_t cus) {
   return ks_stash_rows_bound(rows, cus);
+}
+// host entry points' chunk plans (pipe_plan.hpp): chunk sizes into out (at most maxn), returns the count
+int nth_verify_chunk_targets(unsigned long long total, unsigned long long r1, unsigned long long cap,
+                             unsigned long long* out, int maxn) {
+  const auto t = verify_chunk_targets(total, r1, cap);
+  for (size_t i = 0; i < t.size() && (int)i < maxn; ++i) out[i] = t[i];
+  return (int)t.size();
+}
+int nth_chunk_targets(unsigned long long total, unsigned long long r, unsigned long long cap, int round4,
+                      unsigned long long* out, int maxn) {
+  const auto t = chunk_targets(total, r, cap, round4 != 0);
+  for (size_t i = 0; i < t.size() && (int)i < maxn; ++i) out[i] = t[i];
+  return (int)t.size();
+}
+// certificate-group chunks: groups [0, G) with counts cnt, targets as above; out = chunk ends g1
+int nth_plan_group_chunks(unsigned long long G, const uint32_t* cnt, const unsigned long long* targets, int nt,
+                          unsigned long long* out, int maxn) {
+  const std::vector<uint64_t> tg(targets, targets + nt);
+  const auto r = plan_group_chunks(0, G, cnt, tg);
+  for (size_t i = 0; i < r.size() && (int)i < maxn; ++i) out[i] = r[i].second;
+  return (int)r.size();
 }
 // streamed rows (ks_stream_plan): out = waves, rows, prow, per_simd
 void nth_ks_stream_plan(unsigned long long n, uint32_t cus, uint32_t cap, int force, uint32_t* out) {
