@@ -57,8 +57,8 @@ METRIC = "Ed25519 verifies/sec + SHA-512 GB/s at 1/2/4/8 MI355X vs dalek host-co
 MAD_PEAK_TS = 256 * 4 * 64 * 2.4e9 / 4 / 1e12  # v_mad_u64_u32: 4 cycles per wave64 per SIMD
 MAD_MEASURED_TS = 32.80  # profiles/r01_alu_rate.txt (tools/microbench): 4.80 cycles per wave64 per SIMD
 HBM_PEAK_GBS = 8000.0
-PMC_PROFILE = os.path.join("r04", "pmc_verify_sha.json")  # tools/profile_round.sh + tools/pmc_summarize.py
-PMC_KEYSET_PROFILE = os.path.join("r04", "pmc_keyset.json")  # cfg3 key-cache launch (streamed rows)
+PMC_PROFILE = os.path.join("r05", "pmc_verify_sha.json")  # tools/profile_round.sh + tools/pmc_summarize.py
+PMC_KEYSET_PROFILE = os.path.join("r05", "pmc_keyset.json")  # cfg3 key-cache launch (streamed rows)
 PMC_N = 1_000_000  # signatures per launch in that profile (the default config-2 run)
 SODIUM = "/opt/conda/lib/libsodium.so.23"
 

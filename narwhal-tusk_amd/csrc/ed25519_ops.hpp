@@ -90,9 +90,10 @@ NT_HD NT_INLINE int32_t wcomb_digit(uint32_t d[8], uint32_t& carry) {
 #ifndef NT_COMB_FROM_ID
 #define NT_COMB_FROM_ID 1
 #endif
-template <class WComb, bool kFromIdentity = false>
+template <class WComb, bool kFromIdentity = false, int kSkipTop = 0>
 NT_HD NT_INLINE void wcomb_acc(ge_p3& acc, const uint32_t x[8], const WComb& wc) {
-  constexpr int W = WComb::kBits, P = CombGeom<W>::kPos;
+  // kSkipTop > 0: timing-only experiment builds (wrong results) that drop top positions
+  constexpr int W = WComb::kBits, P = CombGeom<W>::kPos - kSkipTop;
   uint32_t d[8], carry = 0;
 #pragma unroll
   for (int m = 0; m < 8; ++m) d[m] = x[m];
@@ -502,7 +503,11 @@ NT_HD NT_INLINE uint32_t cached_point(ge_p3& acc, uint32_t meta, const uint32_t 
   if (is_strict<MODE>(meta)) okj &= (meta & kKeySmallOrder) ? 0u : 1u;
   uint32_t k[8];
   hram_scalar<true>(k, Rw, Aw, msg, len);
+#ifdef NT_EXPERIMENT_KEY_SKIP
+  wcomb_acc<WCombA, true, NT_EXPERIMENT_KEY_SKIP>(acc, k, ca);  // timing only: wrong verdicts
+#else
   wcomb_acc<WCombA, true>(acc, k, ca);
+#endif
   wcomb_acc(acc, Sw, cb);
   return okj;
 }

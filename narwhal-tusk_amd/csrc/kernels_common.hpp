@@ -59,6 +59,9 @@ struct WideComb {
 #ifdef NT_EXPERIMENT_CACHED_COMB
     idx &= 7;  // timing experiment only (wrong results): every lookup hits in cache
 #endif
+#ifdef NT_EXPERIMENT_BHALF
+    if (W == kBCombBits) idx >>= 1;  // timing experiment only (wrong results): half of each position's table
+#endif
     const uint4* e = (const uint4*)(base + ((size_t)pos * CombGeom<W>::kEntries + idx) * kWStride);
     uint32_t w[32];
 #pragma unroll
