@@ -61,22 +61,34 @@ constexpr int kWChunk = 64;   // consecutive entries built by one thread
 template <int W>
 struct CombGeom {
   static_assert(W >= 12 && W <= 26, "comb digit width");
-  static constexpr int kPos = (254 + W - 1) / W;          // signed digits of a 253-bit scalar
-  static constexpr int kEntries = (1 << (W - 1)) + 1;     // |digit| in 0..2^(W-1)
-  static constexpr int kChunks = (1 << (W - 1)) / kWChunk;  // chunks per position: entries 1..2^(W-1)
-  static constexpr size_t kWordsPerPoint = (size_t)kPos * kEntries * kWStride;
+  // Reduced-scalar combs (W == kKeyCombReduced, committee keys only): the
+  // scalar is k or k - L, whichever is smaller in magnitude (|k'| <= (L - 1) / 2
+  // < 2^251 + 2^124), so ceil(252 / W) digits; the top digit is taken unsigned
+  // (it can reach 2^(W-1) + 1: one more chunk of 64 entries per position), and
+  // the point's [L]P (the torsion part of [k - L]P's error: identity for a
+  // torsion-free point) follows the positions as one niels entry.
+  static constexpr bool kReduced = W == kKeyCombReduced;
+  static constexpr int kPos = kReduced ? (252 + W - 1) / W : (254 + W - 1) / W;  // signed digits of the scalar
+  static constexpr int kChunks = (1 << (W - 1)) / kWChunk + (kReduced ? 1 : 0);  // chunks per position: entries 1..
+  static constexpr int kEntries = kChunks * kWChunk + 1;                         // |digit| in 0..2^(W-1) (+ 64)
+  static constexpr size_t kCorrWord = (size_t)kPos * kEntries * kWStride;        // the [L]P entry (reduced)
+  static constexpr size_t kWordsPerPoint = kCorrWord + (kReduced ? kWStride : 0);
   // the top digit of any x < 2^253 (every scalar of a passing check) never goes
   // negative, so no carry is lost: the bits above (kPos-1) W plus a carry are <= 2^(W-1)
-  static_assert(253 - (kPos - 1) * W <= W - 1, "top comb digit must absorb the carry");
+  static_assert(kReduced || 253 - (kPos - 1) * W <= W - 1, "top comb digit must absorb the carry");
+  // reduced: the top digit (bits (kPos-1) W .. 251 plus a carry) is at most 2^(W-1) + 1
+  static_assert(!kReduced || (252 - (kPos - 1) * W == W && kChunks * kWChunk >= (1 << (W - 1)) + 1),
+                "reduced comb: the unsigned top digit needs its extra chunk");
 };
 
 // Next signed radix-2^W digit of the scalar held in d (d >>= W), in
 // [-2^(W-1)+1, 2^(W-1)] for ANY 256-bit input (an unchecked s >= L only yields
 // a wrong point, never an out-of-range table index; its verdict is reject).
+// top_unsigned: the top digit of a reduced-scalar comb, taken as is (no carry out).
 template <int W>
-NT_HD NT_INLINE int32_t wcomb_digit(uint32_t d[8], uint32_t& carry) {
+NT_HD NT_INLINE int32_t wcomb_digit(uint32_t d[8], uint32_t& carry, bool top_unsigned = false) {
   const uint32_t raw = (d[0] & ((1u << W) - 1u)) + carry;
-  carry = raw > (1u << (W - 1)) ? 1u : 0u;
+  carry = raw > (1u << (W - 1)) && !top_unsigned ? 1u : 0u;
 #pragma unroll
   for (int m = 0; m < 7; ++m) d[m] = (d[m] >> W) | (d[m + 1] << (32 - W));
   d[7] >>= W;
@@ -91,9 +103,11 @@ NT_HD NT_INLINE int32_t wcomb_digit(uint32_t d[8], uint32_t& carry) {
 #define NT_COMB_FROM_ID 1
 #endif
 template <class WComb, bool kFromIdentity = false, int kSkipTop = 0>
-NT_HD NT_INLINE void wcomb_acc(ge_p3& acc, const uint32_t x[8], const WComb& wc) {
+NT_HD NT_INLINE void wcomb_acc(ge_p3& acc, const uint32_t x[8], const WComb& wc, uint32_t neg_all = 0) {
   // kSkipTop > 0: timing-only experiment builds (wrong results) that drop top positions
+  // neg_all: acc += [-x]P (a reduced-scalar comb's k - L < 0): every digit's sign flipped
   constexpr int W = WComb::kBits, P = CombGeom<W>::kPos - kSkipTop;
+  constexpr bool kRed = CombGeom<W>::kReduced;
   uint32_t d[8], carry = 0;
 #pragma unroll
   for (int m = 0; m < 8; ++m) d[m] = x[m];
@@ -102,9 +116,9 @@ NT_HD NT_INLINE void wcomb_acc(ge_p3& acc, const uint32_t x[8], const WComb& wc)
   wc.load(0, (uint32_t)(dg < 0 ? -dg : dg), ne);
   int pos0 = 0;
   if (kFromIdentity && NT_COMB_FROM_ID) {
-    ge_niels_cneg(ne, dg < 0);
+    ge_niels_cneg(ne, (dg < 0) ^ (neg_all != 0));
     ge_p3_from_niels(acc, ne);
-    dg = wcomb_digit<W>(d, carry);
+    dg = wcomb_digit<W>(d, carry, kRed && P == 2);
     wc.load(1, (uint32_t)(dg < 0 ? -dg : dg), ne);
     pos0 = 1;
   } else if (kFromIdentity) {
@@ -112,10 +126,11 @@ NT_HD NT_INLINE void wcomb_acc(ge_p3& acc, const uint32_t x[8], const WComb& wc)
   }
 #pragma unroll 1
   for (int pos = pos0; pos < P; ++pos) {
-    ge_niels_cneg(ne, dg < 0);
+    ge_niels_cneg(ne, (dg < 0) ^ (neg_all != 0));
     fe PP, MM, TT;
     ge_add_niels_1(PP, MM, TT, acc, ne);
-    const int32_t dn = wcomb_digit<W>(d, carry);  // past the last position: a harmless in-range digit
+    // past the last position: a harmless in-range digit
+    const int32_t dn = wcomb_digit<W>(d, carry, kRed && pos + 2 == P);
     const int nxt = pos + 1 < P ? pos + 1 : pos;   // last round reloads a valid entry
     wc.load(nxt, (uint32_t)(dn < 0 ? -dn : dn), ne);
     dg = dn;
@@ -123,6 +138,56 @@ NT_HD NT_INLINE void wcomb_acc(ge_p3& acc, const uint32_t x[8], const WComb& wc)
     ge_add_niels_2(t, PP, MM, TT, acc.Z);
     ge_cp_to_p3(acc, t);
   }
+}
+
+// [L]P as an affine niels entry (the reduced-scalar comb's correction), and
+// whether P has a torsion component ([L]P != identity).  253 doublings and the
+// additions of L's set bits, once per committee key.
+NT_HD NT_INLINE uint32_t wcomb_corr(ge_niels& q, const ge_p3& P) {
+  ge_cached Pc;
+  ge_p3_to_cached(Pc, P);
+  ge_p3 Q;
+  ge_p3_0(Q);
+  ge_cp t;
+#pragma unroll 1
+  for (int bit = 252; bit >= 0; --bit) {
+    ge_p2 q2;
+    ge_p3_to_p2(q2, Q);
+    ge_dbl(t, q2);
+    ge_cp_to_p3(Q, t);
+    if ((kScL[bit >> 5] >> (bit & 31)) & 1u) {
+      ge_add_cached(t, Q, Pc);
+      ge_cp_to_p3(Q, t);
+    }
+  }
+  fe zi;
+  fe_invert(zi, Q.Z);
+  ge_niels_from(q, Q.X, Q.Y, zi);
+  // identity <=> X == 0 and Y == Z
+  return (fe_iszero(Q.X) & fe_eq(Q.Y, Q.Z)) ^ 1u;
+}
+
+// k (< L) -> its magnitude when k - L is the smaller one: returns 1 and sets
+// k = L - k iff k > (L - 1) / 2, so |k'| <= (L - 1) / 2 (reduced-scalar combs)
+NT_HD NT_INLINE uint32_t sc_reduce_half(uint32_t k[8]) {
+  uint32_t t[8];
+  uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {  // t = L - k
+    const uint64_t v = (uint64_t)kScL[i] - k[i] - br;
+    t[i] = (uint32_t)v;
+    br = (v >> 63) & 1u;
+  }
+  // L - k < k  <=>  k > L / 2
+  uint32_t lt = 0, eq = 1;
+#pragma unroll
+  for (int i = 7; i >= 0; --i) {
+    lt |= eq & (t[i] < k[i] ? 1u : 0u);
+    eq &= t[i] == k[i] ? 1u : 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) k[i] = lt ? t[i] : k[i];
+  return lt;
 }
 
 // Wide-comb construction, step 1 (one thread per point): P_i = 2^(W i) P,
@@ -297,6 +362,15 @@ NT_HD NT_INLINE void ptab_build(const ge_p3& P, uint32_t neg, ATab& at, uint32_t
     ge_p3_to_cached(cj, cur);
     at.store(e0 + j, cj);
   }
+#endif
+}
+
+// any lane of the wave (the host: this lane)
+NT_HD NT_INLINE bool wave_any(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ballot(x != 0) != 0;
+#else
+  return x != 0;
 #endif
 }
 
@@ -484,7 +558,9 @@ NT_HD NT_INLINE void verify_n(uint32_t ok[N], const uint32_t* const A[N], const 
 }
 
 // Key-cache variant.  meta = the key's kKey* bits.
-enum : uint32_t { kKeyDecodes = 1u, kKeySmallOrder = 2u };
+// kKeyTorsion: the key has a torsion component ([L]A != identity; reduced-scalar combs add the
+// key's [L](-A) entry when they use k - L)
+enum : uint32_t { kKeyDecodes = 1u, kKeySmallOrder = 2u, kKeyTorsion = 4u };
 // set by the kMixed loader in the meta it hands over: this signature is checked strictly
 constexpr uint32_t kKeyWantStrict = 0x80000000u;
 // strictness of one signature: the mode, or in kMixed mode the loader's per-signature bit
@@ -506,7 +582,25 @@ NT_HD NT_INLINE uint32_t cached_point(ge_p3& acc, uint32_t meta, const uint32_t 
 #ifdef NT_EXPERIMENT_KEY_SKIP
   wcomb_acc<WCombA, true, NT_EXPERIMENT_KEY_SKIP>(acc, k, ca);  // timing only: wrong verdicts
 #else
-  wcomb_acc<WCombA, true>(acc, k, ca);
+  if (CombGeom<WCombA::kBits>::kReduced) {
+    // [k](-A) = [k - L](-A) + [L](-A): one position fewer; the second term is
+    // the identity unless A has a torsion component
+    const uint32_t kneg = sc_reduce_half(k);
+    wcomb_acc<WCombA, true>(acc, k, ca, kneg);
+    const uint32_t corr = kneg & ((meta & kKeyTorsion) ? 1u : 0u);
+    if (wave_any(corr)) {
+      ge_niels c;
+      ca.load_corr(c);
+      if (!corr) ge_niels_0(c);
+      fe PP, MM, TT;
+      ge_add_niels_1(PP, MM, TT, acc, c);
+      ge_cp t;
+      ge_add_niels_2(t, PP, MM, TT, acc.Z);
+      ge_cp_to_p3(acc, t);
+    }
+  } else {
+    wcomb_acc<WCombA, true>(acc, k, ca);
+  }
 #endif
   wcomb_acc(acc, Sw, cb);
   return okj;

@@ -1,0 +1,14 @@
+// k_keyset_mixed_w21.hip -- key-cache kernels, mixed mode (per-signature strictness), 21-bit reduced-scalar key combs, for
+// both widths of the comb of B (one translation unit per mode and key-comb width:
+// the build compiles them in parallel).
+#include "k_keyset.inc"
+
+#define NT_KS_INST(WB)                                                                                          \
+  template hipError_t launch_keyset_m<kMixed, 21, WB>(                                                          \
+      const KsPlan&, const uint32_t*, const uint8_t*, const uint8_t*, uint64_t, const uint64_t*, const uint64_t*,  \
+      uint64_t, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t, const uint32_t*, void*, uint64_t*,  \
+      const uint32_t*, uint8_t*, uint32_t*, hipStream_t);
+namespace nt {
+NT_KS_INST(kBCombBits)
+NT_KS_INST(kBCombFallback)
+}  // namespace nt

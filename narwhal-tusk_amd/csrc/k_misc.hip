@@ -204,9 +204,11 @@ __global__ __launch_bounds__(128) void k_sha512_pipe(const uint8_t* __restrict__
 // One thread per point: decode (or take B), optionally negate, write the
 // kPos bases 2^(W i) P.  meta[key] gets the kKey* bits.  Keys that do not decode get
 // identity bases (every entry the identity; such keys always reject via meta).
+// Reduced-scalar combs (CombGeom::kReduced) also get the point's [L]P entry
+// after their positions and, in meta, kKeyTorsion when it is not the identity.
 template <int W>
 __global__ void k_wcomb_bases(const uint32_t* __restrict__ enc, uint32_t nkeys, int negate,
-                              uint32_t* __restrict__ bases, uint32_t* __restrict__ meta) {
+                              uint32_t* __restrict__ bases, uint32_t* __restrict__ meta, uint32_t* __restrict__ comb) {
   const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
   if (key >= nkeys) return;
   uint32_t w[8];
@@ -214,7 +216,7 @@ __global__ void k_wcomb_bases(const uint32_t* __restrict__ enc, uint32_t nkeys, 
   for (int i = 0; i < 8; ++i) w[i] = enc[8 * key + i];
   ge_p3 P;
   const uint32_t ok = ge_frombytes_w(P, w);
-  if (meta) meta[key] = (ok ? kKeyDecodes : 0u) | (ge_is_small_order(P) ? kKeySmallOrder : 0u);
+  uint32_t m = (ok ? kKeyDecodes : 0u) | (ge_is_small_order(P) ? kKeySmallOrder : 0u);
   if (!ok) ge_p3_0(P);
   if (negate) {
     fe_neg(P.X, P.X);
@@ -222,6 +224,16 @@ __global__ void k_wcomb_bases(const uint32_t* __restrict__ enc, uint32_t nkeys, 
     fe_neg(P.T, P.T);
     fe_carry(P.T);
   }
+  if (CombGeom<W>::kReduced) {
+    ge_niels q;
+    m |= wcomb_corr(q, P) ? kKeyTorsion : 0u;
+    uint32_t* o = comb + (size_t)key * CombGeom<W>::kWordsPerPoint + CombGeom<W>::kCorrWord;
+#pragma unroll
+    for (int l = 0; l < 10; ++l) { o[l] = q.ypx.v[l]; o[10 + l] = q.ymx.v[l]; o[20 + l] = q.xy2d.v[l]; }
+    o[30] = 0;
+    o[31] = 0;
+  }
+  if (meta) meta[key] = m;
   wcomb_bases<W>(bases + (size_t)key * CombGeom<W>::kPos * 40, P);
 }
 
@@ -427,7 +439,7 @@ static hipError_t wcomb_build(const uint32_t* d_enc, uint32_t nkeys, int negate,
                               uint32_t* d_meta, uint32_t* d_bases, uint32_t* d_tmp, uint32_t batch, hipStream_t s) {
   using G = CombGeom<W>;
   hipLaunchKernelGGL(k_wcomb_bases<W>, dim3((nkeys + 63) / 64), dim3(64), 0, s, d_enc, nkeys, negate, d_bases,
-                     d_meta);
+                     d_meta, d_comb);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   for (uint32_t k0 = 0; k0 < nkeys; k0 += batch) {
@@ -447,6 +459,8 @@ hipError_t launch_wcomb_build(int bits, const uint32_t* d_enc, uint32_t nkeys, i
   if (nkeys == 0) return hipSuccess;
   if (batch == 0) return hipErrorInvalidValue;
   switch (bits) {
+    case kKeyCombReduced:
+      return wcomb_build<kKeyCombReduced>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
     case kKeyCombWide: return wcomb_build<kKeyCombWide>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
     case kKeyCombMid: return wcomb_build<kKeyCombMid>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);
     case kBCombBits: return wcomb_build<kBCombBits>(d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s);  // B only
@@ -646,7 +660,8 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
    : mode == kMixed ? launch_keyset_m<kMixed, WA, WB>(NT_KS_ARGS)             \
                     : launch_keyset_m<kCofactorless, WA, WB>(NT_KS_ARGS))
 #define NT_KS_WIDTHS(WB)                                                     \
-  (key_bits == kKeyCombWide     ? NT_KS_MODES(kKeyCombWide, WB)              \
+  (key_bits == kKeyCombReduced  ? NT_KS_MODES(kKeyCombReduced, WB)           \
+   : key_bits == kKeyCombWide   ? NT_KS_MODES(kKeyCombWide, WB)              \
    : key_bits == kKeyCombMid    ? NT_KS_MODES(kKeyCombMid, WB)               \
    : key_bits == kKeyCombNarrow ? NT_KS_MODES(kKeyCombNarrow, WB)            \
                                 : hipErrorInvalidValue)
@@ -675,7 +690,8 @@ static size_t comb_size(int what) {
   }
 }
 static size_t comb_size(int bits, int what) {
-  return bits == kKeyCombWide     ? comb_size<kKeyCombWide>(what)
+  return bits == kKeyCombReduced  ? comb_size<kKeyCombReduced>(what)
+         : bits == kKeyCombWide   ? comb_size<kKeyCombWide>(what)
          : bits == kKeyCombMid    ? comb_size<kKeyCombMid>(what)
          : bits == kKeyCombNarrow ? comb_size<kKeyCombNarrow>(what)
          : bits == kBCombBits     ? comb_size<kBCombBits>(what)

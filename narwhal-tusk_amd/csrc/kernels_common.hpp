@@ -62,6 +62,9 @@ struct WideComb {
 #ifdef NT_EXPERIMENT_BHALF
     if (W == kBCombBits) idx >>= 1;  // timing experiment only (wrong results): half of each position's table
 #endif
+#ifdef NT_EXPERIMENT_KHALF
+    if (W == kKeyCombWide) idx >>= 1;  // timing experiment only (wrong results): half of each key position's table
+#endif
     const uint4* e = (const uint4*)(base + ((size_t)pos * CombGeom<W>::kEntries + idx) * kWStride);
     uint32_t w[32];
 #pragma unroll
@@ -74,6 +77,22 @@ struct WideComb {
 #else
       const uint4 v = e[i];
 #endif
+      w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      q.ypx.v[i] = w[i];
+      q.ymx.v[i] = w[10 + i];
+      q.xy2d.v[i] = w[20 + i];
+    }
+  }
+  // the point's [L]P entry after the positions (reduced-scalar combs, CombGeom::kCorrWord)
+  NT_D NT_INLINE void load_corr(ge_niels& q) const {
+    const uint4* e = (const uint4*)(base + CombGeom<W>::kCorrWord);
+    uint32_t w[32];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint4 v = e[i];
       w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
     }
 #pragma unroll

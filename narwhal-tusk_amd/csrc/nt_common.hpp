@@ -31,7 +31,8 @@ enum VerifyMode : int {
 };
 
 // Digit widths of the committee-key combs (ed25519_ops.hpp, wide combs)
-constexpr int kKeyCombWide = 20;    // 13 additions per [k]A, 872 MB per key: used when they fit in HBM
+constexpr int kKeyCombReduced = 21;  // 12 additions per [k]A (k reduced to |k| <= L/2), 1.61 GB per key: used when they fit
+constexpr int kKeyCombWide = 20;    // 13 additions per [k]A, 872 MB per key
 constexpr int kKeyCombMid = 18;     // 15 additions, 252 MB per key (NT_KEYSET_COMB_BITS=18, A/B)
 constexpr int kKeyCombNarrow = 16;  // 16 additions, 67 MB per key
 
@@ -40,7 +41,10 @@ constexpr int kKeyCombNarrow = 16;  // 16 additions, 67 MB per key
 // device's free memory cannot hold 11.8 GB (ntcrypto.cpp: comb_b_for).  Every
 // kernel that reads it is compiled for both; the launchers dispatch on the width
 // of the comb the device entry holds.
-constexpr int kBCombBits = 24;      // 11 additions per [s]B, 11.8 GB (the host harness builds this one)
+#ifndef NT_BCOMB_WIDE
+#define NT_BCOMB_WIDE 24  // A/B builds: -DNT_BCOMB_WIDE=26 (10 additions, 43 GB)
+#endif
+constexpr int kBCombBits = NT_BCOMB_WIDE;  // 24: 11 additions per [s]B, 11.8 GB (the host harness builds this one)
 constexpr int kBCombFallback = 20;  // 13 additions, 872 MB
 
 // Message i of a launch is msg[off[i] .. off[i] + len[i]) of a buffer of

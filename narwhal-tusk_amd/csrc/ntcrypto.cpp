@@ -1006,20 +1006,21 @@ int nt_ed25519_keypair_batch(nt_ctx* ctx, const uint8_t* seed32, uint64_t n, uin
 }
 
 // ---- committee key cache --------------------------------------------------
-// Comb width of a new key set: the widest of 20 / 18 / 16-bit digits (13 / 15 /
-// 16 additions per [k]A; 872 / 252 / 67 MB per key) that, on every device entry
-// of the context, fits the context's HBM budget beside the comb of B and the
-// tables the entry already holds, and leaves 1/8 of the device's HBM free.
-// With no width passing the free-memory test the 16-bit combs are tried anyway
-// (hipMalloc decides); 0 = not even those fit the budget.
-// NT_KEYSET_COMB_BITS=16|18|20 forces one (18 bits: the A/B width of round 2).
+// Comb width of a new key set: the widest of 21 (reduced scalars) / 20 / 18 /
+// 16-bit digits (12 / 13 / 15 / 16 additions per [k]A; 1.61 GB / 872 / 252 /
+// 67 MB per key) that, on every device entry of the context, fits the
+// context's HBM budget beside the comb of B and the tables the entry already
+// holds, and leaves 1/8 of the device's HBM free.  With no width passing the
+// free-memory test the 16-bit combs are tried anyway (hipMalloc decides); 0 =
+// not even those fit the budget.  NT_KEYSET_COMB_BITS=16|18|20|21 forces one.
 static int keyset_comb_bits(nt_ctx* ctx, uint32_t nkeys) {
   if (const char* e = std::getenv("NT_KEYSET_COMB_BITS")) {
     const int b = std::atoi(e);
-    if (b == nt::kKeyCombWide || b == nt::kKeyCombMid || b == nt::kKeyCombNarrow) return b;
+    if (b == nt::kKeyCombReduced || b == nt::kKeyCombWide || b == nt::kKeyCombMid || b == nt::kKeyCombNarrow)
+      return b;
   }
   const uint64_t nk = std::max<uint32_t>(nkeys, 1);
-  for (const int w : {nt::kKeyCombWide, nt::kKeyCombMid, nt::kKeyCombNarrow}) {
+  for (const int w : {nt::kKeyCombReduced, nt::kKeyCombWide, nt::kKeyCombMid, nt::kKeyCombNarrow}) {
     const uint64_t comb = nt::wcomb_bytes_per_key(w) * nk;
     const uint64_t need = comb + nt::wcomb_fill_tmp_bytes_per_key(w) * nt::wcomb_fill_batch(w);
     bool ok = true;

@@ -26,6 +26,7 @@ def load():
         _lib.nth_wcomb_chunk.restype = ctypes.c_uint32
         _lib.nth_count_mul.restype = ctypes.c_ulonglong
         _lib.nth_count_sq.restype = ctypes.c_ulonglong
+        _lib.nth_key_comb_sum.restype = ctypes.c_uint32
     return _lib
 
 
@@ -92,11 +93,12 @@ def verify_trivial(mode, pk, sig, msg):
     return bool(load().nth_verify_trivial(mode, pk, sig, msg, ctypes.c_uint64(len(msg))))
 
 
-def verify_cached_n(mode, entries, strict_mask=0):
+def verify_cached_n(mode, entries, strict_mask=0, bits=20):
     """1..8 (pk, sig, msg) through the key-cache kernel's path: n signatures per
     lane, one inversion (verify_cached_batch, run-time count n).  mode 2 = mixed:
     entry j is checked strictly iff bit j of strict_mask (the kernel's key_idx
-    bit 31)."""
+    bit 31).  bits: key-comb digit width (20: 13 positions; 21: reduced scalars,
+    12 positions)."""
     n = len(entries)
     assert 1 <= n <= 8
     if mode == 2:
@@ -105,10 +107,22 @@ def verify_cached_n(mode, entries, strict_mask=0):
     msgs = [e[2] for e in entries]
     mp = (ctypes.c_char_p * n)(*msgs)
     lens = (ctypes.c_uint64 * n)(*[len(m) for m in msgs])
-    rc = load().nth_verify_cached_n(mode, n, b"".join(e[0] for e in entries), b"".join(e[1] for e in entries),
-                                    mp, lens, out)
+    rc = load().nth_verify_cached_nw(bits, mode, n, b"".join(e[0] for e in entries), b"".join(e[1] for e in entries),
+                                     mp, lens, out)
     assert rc == 0
     return tuple(bool(x) for x in out)
+
+
+KEY_TORSION = 4  # kKeyTorsion (ed25519_ops.hpp)
+
+
+def key_comb_sum(bits, A: bytes, k: int):
+    """[k](-A) as the key-cache kernel forms it from the key's comb of `bits`-bit
+    digits (21: k reduced to k or k - L, plus the key's [L](-A) entry when k - L
+    was used); returns (encoding, kKey* bits of the key)"""
+    out = ctypes.create_string_buffer(32)
+    meta = load().nth_key_comb_sum(bits, A, k.to_bytes(32, "little"), out)
+    return out.raw, int(meta)
 
 
 def verify_cached4(mode, entries, strict_mask=0):

@@ -39,9 +39,13 @@ template <int W>
 struct HostWComb {
   static constexpr int kBits = W;
   ge_p3 base[CombGeom<W>::kPos];
+  ge_niels corr;       // [L]P (reduced-scalar combs)
+  uint32_t torsion = 0;
   mutable std::unordered_map<uint64_t, ge_niels> memo;
+  void load_corr(ge_niels& q) const { q = corr; }
   void init(const ge_p3& P) {
     const unsigned long long m0 = g_fe_mul, s0 = g_fe_sq;
+    torsion = CombGeom<W>::kReduced ? wcomb_corr(corr, P) : 0u;
     uint32_t w[CombGeom<W>::kPos * 40];
     wcomb_bases<W>(w, P);
     for (int i = 0; i < CombGeom<W>::kPos; ++i)
@@ -91,7 +95,8 @@ struct HostWComb {
 };
 
 using HostBComb = HostWComb<kBCombBits>;
-using HostKeyComb = HostWComb<kKeyCombWide>;  // the device's choice whenever the set fits in HBM
+using HostKeyComb = HostWComb<kKeyCombWide>;        // 13 positions
+using HostKeyCombRed = HostWComb<kKeyCombReduced>;  // 12 positions, reduced scalars: the device's first choice
 
 HostBComb& bcomb() {
   static HostBComb* c = [] {
@@ -107,7 +112,8 @@ HostBComb& bcomb() {
 }
 
 // kKey* bits and the comb of -A, as k_wcomb_bases builds them
-uint32_t key_comb(HostKeyComb& c, const uint32_t Aw[8]) {
+template <class KC>
+uint32_t key_comb(KC& c, const uint32_t Aw[8]) {
   ge_p3 P;
   const uint32_t ok = ge_frombytes_w(P, Aw);
   const uint32_t meta = (ok ? kKeyDecodes : 0u) | (ge_is_small_order(P) ? kKeySmallOrder : 0u);
@@ -117,7 +123,7 @@ uint32_t key_comb(HostKeyComb& c, const uint32_t Aw[8]) {
   fe_neg(P.T, P.T);
   fe_carry(P.T);
   c.init(P);
-  return meta;
+  return meta | (c.torsion ? kKeyTorsion : 0u);
 }
 
 void words(uint32_t w[8], const uint8_t* b) { std::memcpy(w, b, 32); }
@@ -287,38 +293,43 @@ struct HostStash {
   void get_point(int j, ge_p2& p) const { p = P[j]; }
   void get_prefix(int j, fe& a) const { a = pre[j]; }
 };
+}  // extern "C" (the key-cache helpers below are templates)
+template <class KC>
 struct HostCombRef {  // a comb by reference, with the WComb interface
-  static constexpr int kBits = HostKeyComb::kBits;
-  const HostKeyComb* c;
+  static constexpr int kBits = KC::kBits;
+  const KC* c;
   void load(uint32_t pos, uint32_t idx, ge_niels& q) const { c->load(pos, idx, q); }
+  void load_corr(ge_niels& q) const { c->load_corr(q); }
 };
+template <class KC>
 struct HostLoader {
-  using Comb = HostCombRef;
+  using Comb = HostCombRef<KC>;
   const uint32_t (*A)[8];
   const uint32_t (*S)[16];
   const uint8_t* const* M;
   const uint64_t* L;
   const uint32_t* meta;
-  HostKeyComb* ca;
+  KC* ca;
   void get(int j, uint32_t& m, uint32_t Aw[8], uint32_t Rw[8], uint32_t Sw[8], const uint8_t*& msg, uint64_t& len,
            Comb& c) const {
     m = meta[j];
     for (int q = 0; q < 8; ++q) { Aw[q] = A[j][q]; Rw[q] = S[j][q]; Sw[q] = S[j][8 + q]; }
     msg = M[j];
     len = L[j];
-    c = HostCombRef{&ca[j]};
+    c = Comb{&ca[j]};
   }
   void rbytes(int j, uint32_t Rw[8]) const {
     for (int q = 0; q < 8; ++q) Rw[q] = S[j][q];
   }
 };
-int nth_verify_cached_n(int mode, int nsig, const uint8_t* pk, const uint8_t* sig, const uint8_t* const* msgs,
-                        const uint64_t* lens, int* out) {
+template <class KC>
+int verify_cached_impl(int mode, int nsig, const uint8_t* pk, const uint8_t* sig, const uint8_t* const* msgs,
+                       const uint64_t* lens, int* out) {
   if (nsig < 1 || nsig > kHostKsMax) return -1;
   alignas(16) uint32_t A[kHostKsMax][8], S[kHostKsMax][16];
   std::memcpy(A, pk, 32 * nsig);
   std::memcpy(S, sig, 64 * nsig);
-  static HostKeyComb ca[kHostKsMax];
+  static KC ca[kHostKsMax];
   const unsigned long long cm = g_fe_mul, cs = g_fe_sq;  // key-cache build is not per signature
   uint32_t meta[kHostKsMax];
   for (int j = 0; j < nsig; ++j) {
@@ -327,7 +338,7 @@ int nth_verify_cached_n(int mode, int nsig, const uint8_t* pk, const uint8_t* si
   }
   g_fe_mul = cm;
   g_fe_sq = cs;
-  HostLoader ld{A, S, msgs, lens, meta, ca};
+  HostLoader<KC> ld{A, S, msgs, lens, meta, ca};
   HostStash st;
   uint64_t bits;
   if ((mode & 0xff) == kMixed) {  // mode = kMixed | strict_mask << 8 (the kernel's key_idx bit 31)
@@ -340,6 +351,60 @@ int nth_verify_cached_n(int mode, int nsig, const uint8_t* pk, const uint8_t* si
   }
   for (int j = 0; j < nsig; ++j) out[j] = (bits >> j) & 1;
   return 0;
+}
+extern "C" {
+int nth_verify_cached_n(int mode, int nsig, const uint8_t* pk, const uint8_t* sig, const uint8_t* const* msgs,
+                        const uint64_t* lens, int* out) {
+  return verify_cached_impl<HostKeyComb>(mode, nsig, pk, sig, msgs, lens, out);
+}
+// the same through key combs of `bits`-bit digits (20: 13 positions; 21: reduced scalars, 12 positions)
+int nth_verify_cached_nw(int bits, int mode, int nsig, const uint8_t* pk, const uint8_t* sig,
+                         const uint8_t* const* msgs, const uint64_t* lens, int* out) {
+  if (bits == kKeyCombReduced) return verify_cached_impl<HostKeyCombRed>(mode, nsig, pk, sig, msgs, lens, out);
+  if (bits == kKeyCombWide) return verify_cached_impl<HostKeyComb>(mode, nsig, pk, sig, msgs, lens, out);
+  return -1;
+}
+// [k](-A) through the key comb of `bits`-bit digits as the key-cache kernel forms it
+// (cached_point: the reduced comb takes k or k - L and adds [L](-A) when it used k - L);
+// out = the point's canonical encoding, returns the key's kKey* bits
+uint32_t nth_key_comb_sum(int bits, const uint8_t* A32, const uint8_t* k32, uint8_t* out32) {
+  uint32_t Aw[8], k[8];
+  words(Aw, A32);
+  words(k, k32);
+  ge_p3 acc;
+  uint32_t meta = 0;
+  auto finish = [&]() {
+    fe zi, x, y;
+    fe_invert(zi, acc.Z);
+    fe_mul(x, acc.X, zi);
+    fe_mul(y, acc.Y, zi);
+    uint32_t yw[8], xw[8];
+    fe_tobytes_w(yw, y);
+    fe_tobytes_w(xw, x);
+    yw[7] |= (xw[0] & 1u) << 31;
+    std::memcpy(out32, yw, 32);
+  };
+  if (bits == kKeyCombReduced) {
+    static HostKeyCombRed c;
+    meta = key_comb(c, Aw);
+    c.memo.clear();
+    const uint32_t kneg = sc_reduce_half(k);
+    wcomb_acc<HostCombRef<HostKeyCombRed>, true>(acc, k, HostCombRef<HostKeyCombRed>{&c}, kneg);
+    if (kneg && (meta & kKeyTorsion)) {
+      ge_niels q;
+      c.load_corr(q);
+      ge_cp t;
+      ge_add_niels(t, acc, q);
+      ge_cp_to_p3(acc, t);
+    }
+  } else {
+    static HostKeyComb c;
+    meta = key_comb(c, Aw);
+    c.memo.clear();
+    wcomb_acc<HostCombRef<HostKeyComb>, true>(acc, k, HostCombRef<HostKeyComb>{&c});
+  }
+  finish();
+  return meta;
 }
 void nth_verify_cached_pair(int mode, const uint8_t* pk64, const uint8_t* sig128, const uint8_t* m0, uint64_t l0,
                             const uint8_t* m1, uint64_t l1, int* out2) {

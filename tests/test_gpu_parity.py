@@ -218,11 +218,14 @@ def test_batch_corpus_rule(be, corpus):
 
 
 # ------------------------------------------------------------------ committee key cache
-@pytest.mark.parametrize("bits", [16, 20])
+@pytest.mark.parametrize("bits", [16, 20, 21])
 def test_keyset_corpus(be, corpus, bits, monkeypatch):
-    """Every corpus key (incl. off-curve, small-order, non-canonical) as a keyset
-    entry, through both key-comb widths (NT_KEYSET_COMB_BITS forces one; the
-    20-bit combs take 872 MB per key, so those sets hold 48 keys at a time)."""
+    """Every corpus key (incl. off-curve, small-order, non-canonical, mixed-order)
+    as a keyset entry, through the key-comb widths (NT_KEYSET_COMB_BITS forces
+    one; the 20-bit combs take 872 MB per key, the 21-bit reduced-scalar combs
+    1.61 GB -- those sets hold 48 keys at a time).  At 21 bits every corpus
+    scalar k is taken as k or k - L, and keys with a torsion component add
+    their [L](-A) entry when k - L was used."""
     import ntcrypto
     monkeypatch.setenv("NT_KEYSET_COMB_BITS", str(bits))
     uniq, inv = np.unique(corpus["pk"], axis=0, return_inverse=True)
@@ -254,13 +257,14 @@ def test_keyset_corpus(be, corpus, bits, monkeypatch):
 
 
 def test_keyset_comb_width_choice(be):
-    """Without an override a committee that fits gets 20-bit combs; the size
+    """Without an override a committee that fits gets 21-bit reduced-scalar
+    combs (12 positions of 2^20 + 65 entries and the [L](-A) entry); the size
     nt_keyset_info reports is the comb bytes of every key."""
     pks = be.sign_batch(np.arange(4 * 32, dtype=np.uint8).reshape(4, 32))
     ks = be.keyset(pks)
     bits, nbytes = ks.info()
-    assert bits == 20
-    assert nbytes >= 4 * 13 * ((1 << 19) + 1) * 128
+    assert bits == 21
+    assert nbytes >= 4 * (12 * ((1 << 20) + 65) + 1) * 128
     ks.close()
 
 

@@ -172,6 +172,61 @@ def test_corpus_through_keyset_path():
             assert H.verify_cached_n(2, [entry(j) for j in idx], strict_mask=mask) == want, (i, "mixed", mask)
 
 
+@pytest.mark.parametrize("bits", [21])
+def test_corpus_through_reduced_key_combs(bits):
+    """The same corpus through 21-bit key combs (the device's first choice): k
+    taken as k or k - L, 12 positions, and the key's [L](-A) entry added when
+    k - L was used -- small-order and mixed-order keys included, every mode."""
+    d = np.load(os.path.join(GOLD, "ed25519_corpus.npz"))
+    n = len(d["cat"])
+
+    def entry(i):
+        o, ln = int(d["off"][i]), int(d["len"][i])
+        return d["pk"][i].tobytes(), d["sig"][i].tobytes(), d["msg"][o:o + ln].tobytes()
+
+    for i in range(0, n, 8):
+        idx = [(i + k) % n for k in range(8)]
+        for mode, key in ((0, "strict"), (1, "batch_rule")):
+            want = tuple(bool(d[key][j]) for j in idx)
+            assert H.verify_cached_n(mode, [entry(j) for j in idx], bits=bits) == want, (i, mode)
+        mask = (i * 37 // 8) % 256
+        want = tuple(bool(d["strict" if (mask >> k) & 1 else "batch_rule"][j]) for k, j in enumerate(idx))
+        assert H.verify_cached_n(2, [entry(j) for j in idx], strict_mask=mask, bits=bits) == want, (i, "mixed")
+
+
+def test_reduced_comb_sum_equals_full_comb():
+    """[k](-A) from the 21-bit reduced-scalar comb equals the 20-bit comb's for
+    honest, small-order and mixed-order keys of the corpus and for scalars at
+    the reduction's edges ((L - 1) / 2, (L + 1) / 2, L - 1, 0, 1, 2^251 +- 1) and
+    random ones; the key's torsion flag is set exactly for keys with a torsion
+    component (the corpus's small- and mixed-order categories but the identity)."""
+    d = np.load(os.path.join(GOLD, "ed25519_corpus.npz"))
+    meta = json.load(open(os.path.join(GOLD, "ed25519_corpus.json")))
+    cats = meta["categories"]
+    rng = np.random.default_rng(21)
+    L = H.L
+    edges = [0, 1, 2, (L - 1) // 2, (L + 1) // 2, (L + 3) // 2, L - 1, L - 2, (1 << 251) - 1, 1 << 251,
+             (1 << 251) + 1, (1 << 252) - 1]
+    seen = {}
+    for i in range(len(d["cat"])):
+        cat = cats[int(d["cat"][i])]
+        if cat not in ("honest", "small_order_A", "mixed_A_valid") or seen.get(cat, 0) >= 6:
+            continue
+        seen[cat] = seen.get(cat, 0) + 1
+        A = d["pk"][i].tobytes()
+        ks = edges + [int.from_bytes(rng.integers(0, 256, 32, dtype=np.uint8).tobytes(), "little") % L
+                      for _ in range(24)]
+        for k in ks:
+            e21, m21 = H.key_comb_sum(21, A, k)
+            e20, m20 = H.key_comb_sum(20, A, k)
+            assert e21 == e20, (cat, i, k)
+            # the identity (y = 1, either sign bit) is small order without a torsion component
+            ident = A[0] == 1 and not any(A[1:31]) and A[31] in (0, 0x80)
+            assert bool(m21 & H.KEY_TORSION) == (cat != "honest" and not ident), (cat, i)
+            assert (m21 & ~H.KEY_TORSION) == m20
+    assert set(seen) == {"honest", "small_order_A", "mixed_A_valid"}
+
+
 def test_sc_halfsize_lehmer_equals_one_step():
     """The Lehmer-batched reduction the kernels run lands on exactly the
     (u, v, sign, bits) of the one-step Euclid loop: random k < L, k near L,
