@@ -1127,9 +1127,11 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                           "keyset_one_stream: the same launches strictly back to back on one stream",
             "key_cache": {"comb_bits": ks_bits, "gb_per_device": round(ks_bytes / 1e9, 2),
                           "build_s": round(ks_build_s, 3),
-                          "note": "per-key wide combs of -A (13 comb additions per [k]A at 20 bits; [s]B: 11 "
+                          "note": "per-key wide combs of -A (%d comb additions per [k]A at %d bits%s; [s]B: 11 "
                                   "additions from the device's 24-bit comb of B), built once "
-                                  "per committee on every device; not in the timed region",
+                                  "per committee on every device; not in the timed region"
+                                  % ({21: 12, 20: 13, 18: 15, 16: 16}.get(ks_bits, 0), ks_bits,
+                                     ", k taken as k or k - L" if ks_bits == 21 else ""),
                           "launches": "per step: SHA-512 of the certificate digests, 1 NT_MODE_MIXED key-cache verify "
                                       "(67 votes cofactorless + the header signature strict), SHA-512 of the header "
                                       "ids (only the verdict needs them), 1 group AND"},

@@ -139,12 +139,13 @@ int nt_ed25519_keypair_batch(nt_ctx *ctx, const uint8_t *seed32, uint64_t n, uin
 
 /* ---- committee key cache ------------------------------
  * A keyset holds, on every device of the context, per-key comb tables
- * (the wide comb of -A: 20-bit digits, 13 x 524289 affine niels entries =
- * 872 MB per key -- 87 GB for n = 100 -- when every device can hold them
- * with 1/8 of its HBM to spare and the context's HBM budget allows, else
- * 18-bit digits, 15 x 131073 entries = 252 MB per key, else 16-bit digits,
- * 16 x 32769 entries = 67 MB per key; NT_KEYSET_COMB_BITS=16|18|20 forces
- * one) plus each key's raw
+ * (the wide comb of -A: 21-bit digits of the scalar reduced to |k| <= L/2,
+ * 12 x 1048641 affine niels entries plus the key's [L](-A) = 1.61 GB per key
+ * -- 161 GB for n = 100 -- when every device can hold them with 1/8 of its
+ * HBM to spare and the context's HBM budget allows, else 20-bit digits, 13 x
+ * 524289 entries = 872 MB per key, else 18-bit digits, 15 x 131073 = 252 MB,
+ * else 16-bit digits, 16 x 32769 = 67 MB; NT_KEYSET_COMB_BITS=16|18|20|21
+ * forces one) plus each key's raw
  * encoding and decode / small-order flags, so verification against a static
  * committee (config/src/lib.rs:140-143) needs no decompression of A and no
  * doublings.  Keys are addressed by index (the caller's committee order);

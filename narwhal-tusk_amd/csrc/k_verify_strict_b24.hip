@@ -3,7 +3,7 @@
 #include "k_verify.inc"
 
 namespace nt {
-template hipError_t launch_verify_m<kStrict, 24>(uint64_t, const uint8_t*, const uint8_t*, const uint8_t*, uint64_t,
+template hipError_t launch_verify_m<kStrict, kBCombBits>(uint64_t, const uint8_t*, const uint8_t*, const uint8_t*, uint64_t,
                                               const uint64_t*, const uint64_t*, uint64_t, const uint32_t*, void*,
                                               uint64_t*, hipStream_t, int);
 }  // namespace nt
