@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
@@ -553,6 +554,56 @@ int run_chunks(Device& dv, size_t C, bool async, Copy&& copy, Launch&& launch) {
   return NT_OK;
 }
 
+// run_chunks for sources that need host staging (a memcpy into the pinned
+// buffers before the DMA): a helper thread stages and issues the copies of every
+// chunk in order, running ahead of the launches, while this thread waits for each
+// chunk's copies and launches its kernels -- the staging of chunk c+1 overlaps
+// both chunk c's DMA and its kernels, and no launch waits behind a memcpy.  The
+// copy callbacks run on the helper thread only (they must not share mutable
+// state with the launch callbacks).
+template <class Copy, class Launch>
+int run_chunks_staged(Device& dv, size_t C, Copy&& copy, Launch&& launch) {
+  if (C <= 1) return run_chunks(dv, C, false, copy, launch);
+  if (C > (size_t)kMaxChunks) return NT_EINVAL;
+  const bool tr = pipe_trace();
+  const double t0 = tr ? pipe_now_us() : 0.0;
+  int hip_dev = 0;
+  NT_TRY(hipGetDevice(&hip_dev));
+  std::mutex mu;
+  std::condition_variable cv;
+  size_t issued = 0;
+  int err = NT_OK;
+  std::thread helper([&] {
+    int rc = hipSetDevice(hip_dev) == hipSuccess ? NT_OK : NT_EHIP;
+    for (size_t c = 0; c < C && rc == NT_OK; ++c) {
+      rc = copy(c);
+      if (rc == NT_OK && hipEventRecord(dv.cev[c], dv.cstream) != hipSuccess) rc = NT_EHIP;
+      if (tr && rc == NT_OK) std::fprintf(stderr, "[pipe] %9.1f copies %zu staged+issued\n", pipe_now_us() - t0, c);
+      std::lock_guard<std::mutex> lk(mu);
+      if (rc == NT_OK) ++issued;
+      else err = rc;
+      cv.notify_one();
+    }
+  });
+  int rc = NT_OK;
+  for (size_t c = 0; c < C && rc == NT_OK; ++c) {
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return issued > c || err != NT_OK; });
+      if (issued <= c) break;  // the helper failed before issuing chunk c
+    }
+    if (hipEventSynchronize(dv.cev[c]) != hipSuccess) {
+      rc = NT_EHIP;
+      break;
+    }
+    if (tr) std::fprintf(stderr, "[pipe] %9.1f copies %zu done\n", pipe_now_us() - t0, c);
+    rc = launch(c);
+    if (tr) std::fprintf(stderr, "[pipe] %9.1f kernels %zu launched\n", pipe_now_us() - t0, c);
+  }
+  helper.join();
+  return rc != NT_OK ? rc : err;
+}
+
 // both compute streams drained (host-side), so work issued next on dv.stream
 // follows every chunk's kernels without a cross-queue wait
 int finish_chunks(Device& dv) {
@@ -871,10 +922,18 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
     uint8_t* hsig = dv.h[B_SIG].as<uint8_t>();
     uint64_t* hfirst = dv.h[B_FIRST].as<uint64_t>();
     uint32_t* hcnt = dv.h[B_CNT].as<uint32_t>();
+    // header digests from pageable memory go through the pinned staging too (32 B
+    // per group): a copy from pageable memory returns only when it is done
+    const bool msg_direct = is_pinned(msg32 + 32 * glo, 32 * gm);
+    NT_CHK(dv.h[B_DATA].ensure(msg_direct ? 1 : gm * 32));
+    uint8_t* hmsg = dv.h[B_DATA].as<uint8_t>();
     hipStream_t cs = dv.cstream;
     NT_TRY(hipMemsetAsync(dv.d[B_OUT].p, 0, sw * 8 + 8, cs));  // before chunk 0's copy-done event
-    // staged groups are in the library's pinned staging; direct ones in the caller's
-    NT_CHK(run_chunks(dv, C, is_pinned(msg32 + 32 * glo, 32 * gm), [&](size_t c) -> int {
+    // direct: every copy is a DMA from pinned memory, so chunk c+1's copies are
+    // queued before the host waits on chunk c; staged: a helper thread stages
+    // (host memcpy of keys and signatures) and issues the chunks ahead of the
+    // launches (run_chunks_staged)
+    auto copy = [&](size_t c) -> int {
       const uint64_t g0 = ch[c].first, g1 = ch[c].second, gl = g0 - glo, e0 = E[c], mc = E[c + 1] - E[c];
       // chunk-local: hfirst relative to e0; message offsets 32 * (g - g0) made on the device
       stage_groups(g0, g1, first, cnt, kw, keys, sig64, hkey + kw * e0, hsig + 64 * e0, hfirst + gl, hcnt + gl,
@@ -885,12 +944,17 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
         NT_TRY(hipMemcpyAsync(dv.d[B_PK].as<uint8_t>() + kw * e0, sk, mc * kw, hipMemcpyHostToDevice, cs));
         NT_TRY(hipMemcpyAsync(dv.d[B_SIG].as<uint8_t>() + 64 * e0, ss, mc * 64, hipMemcpyHostToDevice, cs));
       }
-      NT_TRY(hipMemcpyAsync(dv.d[B_DATA].as<uint8_t>() + 32 * gl, msg32 + 32 * g0, (g1 - g0) * 32,
-                            hipMemcpyHostToDevice, cs));
+      const uint8_t* sm = msg32 + 32 * g0;
+      if (!msg_direct) {
+        std::memcpy(hmsg + 32 * gl, sm, (g1 - g0) * 32);
+        sm = hmsg + 32 * gl;
+      }
+      NT_TRY(hipMemcpyAsync(dv.d[B_DATA].as<uint8_t>() + 32 * gl, sm, (g1 - g0) * 32, hipMemcpyHostToDevice, cs));
       NT_TRY(hipMemcpyAsync(dv.d[B_FIRST].as<uint64_t>() + gl, hfirst + gl, (g1 - g0) * 8, hipMemcpyHostToDevice, cs));
       NT_TRY(hipMemcpyAsync(dv.d[B_CNT].as<uint32_t>() + gl, hcnt + gl, (g1 - g0) * 4, hipMemcpyHostToDevice, cs));
       return NT_OK;
-    }, [&](size_t c) -> int {
+    };
+    auto launch = [&](size_t c) -> int {
       const uint64_t g0 = ch[c].first, g1 = ch[c].second, gl = g0 - glo, e0 = E[c], mc = E[c + 1] - E[c];
       hipStream_t s = dv.cstr((int)c);
       const uint8_t* dk = dv.d[B_PK].as<uint8_t>() + kw * e0;
@@ -918,7 +982,8 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
       NT_TRY(nt::launch_group_and(dv.d[B_FIRST].as<uint64_t>() + gl, dv.d[B_CNT].as<uint32_t>() + gl, g1 - g0, dout,
                                   dv.d[B_OUT2].as<uint64_t>() + gl / 64, s));
       return NT_OK;
-    }));
+    };
+    NT_CHK(direct || m == 0 ? run_chunks(dv, C, true, copy, launch) : run_chunks_staged(dv, C, copy, launch));
     hipStream_t s = dv.stream;
     NT_CHK(finish_chunks(dv));
     NT_TRY(hipMemcpyAsync(dv.h[B_OUT2].p, dv.d[B_OUT2].p, gw * 8, hipMemcpyDeviceToHost, s));

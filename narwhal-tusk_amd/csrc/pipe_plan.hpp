@@ -50,6 +50,33 @@ inline std::vector<uint64_t> verify_chunk_targets(uint64_t total, uint64_t R1, u
 // rest last) for A/B (round4).
 inline std::vector<uint64_t> chunk_targets(uint64_t total, uint64_t R, uint64_t cap, bool round4 = false) {
   if (cap <= 1 || total <= R) return {total};
+  if (!round4 && cap >= 6 && total >= 2 * R) {
+    // A ramp at both ends (R/8, R/4, R/2 ... R/2, R/4, <= R/8).  When a chunk's
+    // copy takes about as long as its kernels (the key-cache kernel verifies
+    // ~0.85 M signatures/ms, PCIe moves ~0.85 M of its 68-B items/ms), chunk c+1
+    // must be no bigger than about chunk c, or the GPU idles while it copies;
+    // and what runs after the last copy lands is one short launch.
+    auto w = [](uint64_t x) { return std::max<uint64_t>(64, x / 64 * 64); };
+    const uint64_t e = w(R / 8), q = w(R / 4), h = w(R / 2);
+    std::vector<uint64_t> t{e, q, h};
+    const uint64_t head = e + q + h;
+    const uint64_t s3 = std::max(head + q, (total - std::min(e, total) + 63) / 64 * 64);  // the last chunk
+    const uint64_t s2 = s3 - q;                                                          // R/4 before it
+    const uint64_t mid = s2 - head;
+    if (mid) {
+      const uint64_t n = std::min(cap - 5, (mid + h - 1) / h);
+      const uint64_t per = (mid + n - 1) / n + 63;
+      uint64_t left = mid;
+      while (left > 0) {
+        const uint64_t c = std::min(per / 64 * 64, left);
+        t.push_back(c);
+        left -= c;
+      }
+    }
+    t.push_back(q);
+    if (total > s3) t.push_back(total - s3);
+    return t;
+  }
   if (!round4 && cap >= 3) {
     const uint64_t q = std::max<uint64_t>(64, R / 4 / 64 * 64);
     std::vector<uint64_t> t{q};

@@ -93,3 +93,26 @@ def test_group_chunks_whole_words():
             ends = list(out[:n])
             assert ends[-1] == G and n <= len(tgt)
             assert all(e % 64 == 0 for e in ends[:-1]) and ends == sorted(ends)
+
+
+@pytest.mark.parametrize("total", [2 * 393216, 2 * 393216 + 1, 3_000_000, 6_700_000, 6_800_000, 20_000_000, 100_000_000])
+def test_chunk_plan_ramp(total):
+    """key-cache / group plans ramp at both ends: R/8, R/4, R/2, middle chunks of
+    about R/2 (bigger only when the 16-chunk cap needs it), R/4, at most R/8 last"""
+    r = 1572864
+    if total < 2 * r:
+        r = 393216
+    t = chunks(total, r, 16)
+    check_boundaries(t, total, 16)
+    assert t[:3] == [r // 8, r // 4, r // 2]
+    assert t[-1] <= r // 8 and (t[-2] == r // 4 or t[-1] == r // 4)
+    mids = t[3:-2] if t[-2] == r // 4 else t[3:-1]
+    if total <= 11 * r // 2 + 5 * r // 4:  # 11 middle chunks of R/2 fit the cap
+        assert all(m <= r // 2 + 64 for m in mids)
+    assert max(mids) - min(mids) <= 64 or len(mids) <= 1 or mids[-1] < mids[0]
+
+
+def test_chunk_plan_config3():
+    """config 3's 6.8M signatures at one key-cache round of 1,572,864"""
+    t = chunks(6_800_000, 1572864)
+    assert t[:3] == [196608, 393216, 786432] and t[-2:] == [393216, 196608] and len(t) == 12

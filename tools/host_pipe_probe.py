@@ -1,9 +1,11 @@
-"""The host entry point's copy/kernel pipeline on config 2 (VERDICT r04 item
-6): nt_ed25519_verify_strict on 1M 512-B verifies from nt_host_alloc (pinned)
-buffers, timed per call; run it under `rocprofv3 --kernel-trace
---memory-copy-trace` to see the chunk timeline.  Prints one JSON line.
+"""The host entry points' copy/kernel pipeline: config 2
+= nt_ed25519_verify_strict on 1M 512-B verifies, config 3 (--cfg3) =
+nt_ed25519_verify_batch_groups_keyset on 100k certificates x 67 votes of a
+100-key committee, from nt_host_alloc (pinned) and pageable buffers, timed per
+call; run it under `rocprofv3 --kernel-trace --memory-copy-trace` or with
+NT_PIPE_TRACE=1 to see the chunk timeline.  Prints one JSON line.
 
-    python tools/host_pipe_probe.py [--sigs 1000000] [--reps 5]
+    python tools/host_pipe_probe.py [--sigs 1000000] [--reps 5] [--cfg3]
 """
 import argparse
 import json
@@ -21,7 +23,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sigs", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--cfg3", action="store_true")
     a = ap.parse_args()
+    if a.cfg3:
+        return cfg3(a)
     import ntcrypto
     be = ntcrypto.Backend(devices=[0])
     rng = np.random.default_rng(3)
@@ -48,6 +53,38 @@ def main():
         t = float(np.median(ts))
         out[name] = {"ms": round(t * 1e3, 3), "per_s": round(n / t, 1), "all_ms": [round(x * 1e3, 2) for x in ts]}
     print(json.dumps(out), flush=True)
+    be.close()
+
+
+def cfg3(a, C=100_000, V=67, nk=100):
+    import ntcrypto
+    be = ntcrypto.Backend(devices=[0])
+    rng = np.random.default_rng(4)
+    kseeds = rng.integers(0, 256, (nk, 32), dtype=np.uint8)
+    msg32 = rng.integers(0, 256, (C, 32), dtype=np.uint8)
+    kidx = np.stack([rng.choice(nk, V, replace=False) for _ in range(C)]).astype(np.uint32).ravel()
+    gmsg = np.repeat(msg32, V, axis=0).ravel()
+    _, gsig = be.sign_batch(kseeds[kidx], gmsg, np.arange(C * V, dtype=np.uint64) * 32, np.full(C * V, 32, np.uint64))
+    ks = be.keyset(be.sign_batch(kseeds))
+    first = np.arange(C, dtype=np.uint64) * V
+    cnt = np.full(C, V, np.uint32)
+    key_p, sig_p = be.pinned((C * V,), np.uint32), be.pinned((C * V, 64))
+    key_p[...] = kidx
+    sig_p[...] = gsig
+    out = {"certificates": C, "votes": V, "comb_bits": ks.info()[0]}
+    for name, args in (("pinned", (key_p, sig_p)), ("pageable", (kidx, gsig))):
+        ks.verify_batch_groups(args[0], args[1], first, cnt, msg32)
+        ts = []
+        for _ in range(a.reps):
+            print("[probe] %s call" % name, file=sys.stderr, flush=True)
+            t0 = time.perf_counter()
+            r = ks.verify_batch_groups(args[0], args[1], first, cnt, msg32)
+            ts.append(time.perf_counter() - t0)
+        assert r.all()
+        t = float(np.median(ts))
+        out[name] = {"ms": round(t * 1e3, 3), "certs_per_s": round(C / t, 1), "all_ms": [round(x * 1e3, 2) for x in ts]}
+    print(json.dumps(out), flush=True)
+    ks.close()
     be.close()
 
 
