@@ -1143,9 +1143,11 @@ def bench_cert_host_api(be, ks, vkey, vsig, cdig, G, quorum, expect, barrier, ma
     """Config 3's votes through nt_ed25519_verify_batch_groups_keyset from pinned
     host buffers: G certificates x `quorum` votes, keys as
     committee indices, one 32-byte certificate digest per group.  The library
-    stages nothing (the inputs are nt_host_alloc memory and densely packed):
-    chunk c+1's copies run under chunk c's key-cache launch on the library's two
-    compute streams.  Verdicts checked against the expected group results."""
+    DMAs keys and signatures straight from them (nt_host_alloc memory, densely
+    packed; only the 32-B digests are memcpy'd into its pinned staging): chunk
+    c+1's copies run under chunk c's key-cache launch on the library's two
+    compute streams, chunks ramped R/8, R/4, R/2 ... R/2, R/4, R/8
+    (pipe_plan.hpp).  Verdicts checked against the expected group results."""
     key_p = be.pinned((G * quorum,), np.uint32)
     sig_p = be.pinned((G * quorum, 64))
     key_p[...] = vkey.cpu().numpy().view(np.uint32)
@@ -1166,7 +1168,7 @@ def bench_cert_host_api(be, ks, vkey, vsig, cdig, G, quorum, expect, barrier, ma
             "ms_per_call": round(wall * 1e3, 3), "mismatches_vs_expected": mism,
             "bytes_per_call": int(G * quorum * 68 + G * 44),
             "note": "nt_ed25519_verify_batch_groups_keyset on %d certificates x %d votes per rank from nt_host_alloc "
-                    "buffers (4-B key index + 64-B signature per vote over PCIe; no staging copy), the library's "
+                    "buffers (4-B key index + 64-B signature per vote over PCIe, no staging copy of them), the library's "
                     "chunk pipeline on its own streams; PCIe-inclusive, never `value`" % (G, quorum)}
 
 
