@@ -627,7 +627,9 @@ NT_HD NT_INLINE uint32_t compare_one(const ge_p2& P, const fe& zi, const uint32_
 #define NT_INV_VT 1
 #endif
 NT_HD NT_INLINE void fe_invert_batch(fe& out, const fe& z) {
-#if NT_INV_VT
+#if defined(NT_EXPERIMENT_NO_INV)
+  out = z;  // timing only (wrong verdicts): what the batch inversion costs a launch
+#elif NT_INV_VT
   fe_invert_vt(out, z);
 #else
   fe_invert(out, z);
