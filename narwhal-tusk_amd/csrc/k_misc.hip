@@ -46,6 +46,7 @@ NT_D NT_INLINE void sha512_put(uint32_t* __restrict__ out, uint64_t i, const uin
   o[1] = make_uint4(w[4], w[5], w[6], w[7]);
   if (!ok && bad) atomicAdd(bad, 1u);
 }
+template <bool kOneSite>
 NT_D NT_INLINE void sha512_trunc32_one(const uint8_t* __restrict__ data, uint64_t data_bytes,
                                        const uint64_t* __restrict__ off, const uint64_t* __restrict__ len, uint64_t n,
                                        uint32_t* __restrict__ out, uint32_t* __restrict__ bad) {
@@ -53,7 +54,8 @@ NT_D NT_INLINE void sha512_trunc32_one(const uint8_t* __restrict__ data, uint64_
   if (i >= n) return;
   const MsgSlice ms = msg_slice(off[i], len[i], data_bytes);
   uint64_t st[8];
-  sha512_prefixed<0>(st, nullptr, data + ms.off, ms.len);
+  if (kOneSite) sha512_prefixed_1site<0>(st, nullptr, data + ms.off, ms.len);
+  else sha512_prefixed<0>(st, nullptr, data + ms.off, ms.len);
   sha512_put(out, i, st, ms.ok, bad);
 }
 __global__ __launch_bounds__(kBlock) void k_sha512_trunc32(const uint8_t* __restrict__ data, uint64_t data_bytes,
@@ -62,27 +64,30 @@ __global__ __launch_bounds__(kBlock) void k_sha512_trunc32(const uint8_t* __rest
                                                           uint64_t n, uint32_t* __restrict__ out,
                                                           uint32_t* __restrict__ bad) {
   aux_priority();
-  sha512_trunc32_one(data, data_bytes, off, len, n, out, bad);
+  sha512_trunc32_one<false>(data, data_bytes, off, len, n, out, bad);
 }
-// The same for short messages (<= kLeanMaxLen bytes) in at most 64 VGPRs (8
-// waves per SIMD; the compression spills ~476 B per lane): beside two
-// co-resident key-cache launches (4 x 112 VGPRs per SIMD) only 64 are free
-// (tools/microbench/co_dispatch.hip).  Off by default: the
-// 8-GPU shard measured 11.31 M certificates/s with it against 11.43 without
-// (round 4, profiles/r04/ab_r04u/); -DNT_SHA_LEAN_MAX=256 builds it in (A/B).
+// The same in at most 80 VGPRs (6 waves per SIMD; one compression site, ~184 B
+// of spills per lane) against the general kernel's 165, for launches of at most
+// kLeanMaxMsgs messages (one wave per SIMD of a 256-CU device): such a launch is
+// latency-bound, and beside a key-cache launch of two waves per SIMD (2 x 216 of
+// a SIMD's 512 VGPRs) the 80-VGPR kernel is placed at once instead of after that
+// launch's waves exit -- config 3's shards run the header-id digests (12.5k -
+// 50k x 3.3 KB, side streams) beside the other stream's key-cache launch.
+// Larger launches keep the general kernel: the full config-3 step's 100k header
+// digests ran ~1 % slower spilling (profiles/r05/ab_sha_lean_r05.txt).
+// NT_SHA_LEAN_MSGS overrides the bound (0: never); -DNT_SHA_LEAN_MAX=0 builds it out.
 #ifndef NT_SHA_LEAN_MAX
-#define NT_SHA_LEAN_MAX 0
+#define NT_SHA_LEAN_MAX 1
 #endif
-[[maybe_unused]] constexpr uint64_t kLeanMaxLen = NT_SHA_LEAN_MAX;
 #if NT_SHA_LEAN_MAX > 0
-__global__ __launch_bounds__(kBlock, 8) void k_sha512_trunc32_lean(const uint8_t* __restrict__ data,
+__global__ __launch_bounds__(kBlock, 6) void k_sha512_trunc32_lean(const uint8_t* __restrict__ data,
                                                                    uint64_t data_bytes,
                                                                    const uint64_t* __restrict__ off,
                                                                    const uint64_t* __restrict__ len,
                                                                    uint64_t n, uint32_t* __restrict__ out,
                                                                    uint32_t* __restrict__ bad) {
   aux_priority();
-  sha512_trunc32_one(data, data_bytes, off, len, n, out, bad);
+  sha512_trunc32_one<true>(data, data_bytes, off, len, n, out, bad);
 }
 #endif
 
@@ -355,7 +360,8 @@ hipError_t launch_sha512_trunc32(const uint8_t* d_data, uint64_t data_bytes, con
   }
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
 #if NT_SHA_LEAN_MAX > 0
-  if (max_len <= kLeanMaxLen) {
+  static const uint64_t lean_max = (uint64_t)env_occ("NT_SHA_LEAN_MSGS", 65536, 0, 1 << 30);
+  if (n <= lean_max) {
     hipLaunchKernelGGL(k_sha512_trunc32_lean, dim3((uint32_t)blocks), dim3(kBlock), 0, s, d_data, data_bytes, d_off,
                        d_len, n, (uint32_t*)d_out32, d_bad);
     return hipGetLastError();

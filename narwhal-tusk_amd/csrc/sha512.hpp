@@ -362,6 +362,25 @@ NT_HD NT_INLINE void sha512_prefixed(uint64_t st[8], const uint32_t* prefix, con
   }
 }
 
+// The same with one compression site (full and tail blocks chosen per block):
+// about half the code of sha512_prefixed, for kernels built on a tight register
+// budget (k_sha512_trunc32 at 80 VGPRs).
+template <int PW>
+NT_HD NT_INLINE void sha512_prefixed_1site(uint64_t st[8], const uint32_t* prefix, const uint8_t* msg,
+                                           uint64_t len) {
+  sha512_init(st);
+  const uint64_t total = (uint64_t)(4 * PW) + len;
+  const uint64_t nblocks = (total + 17 + 127) / 128;
+  const uint64_t nfull = total / 128;
+#pragma unroll 1
+  for (uint64_t b = 0; b < nblocks; ++b) {
+    uint32_t blk[32];
+    if (b < nfull && (PW == 0 || b > 0)) load_words<32>(blk, msg + (128 * b - 4 * PW));
+    else sha512_tail_block<PW>(blk, prefix, msg, len, b, b == nblocks - 1);
+    sha512_compress_words(st, blk);
+  }
+}
+
 // k = H(R || A || M) for a 32-byte M (every key-cache signature: headers, votes and
 // certificates sign a 32-byte digest, crypto/src/lib.rs:185-204): the 96 bytes
 // are one block built straight from registers -- no byte-granular tail assembly

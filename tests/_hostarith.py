@@ -178,9 +178,9 @@ def sc_reduce512(b):
     return o.raw
 
 
-def sha512(m):
+def sha512(m, one_site=False):
     o = ctypes.create_string_buffer(64)
-    load().nth_sha512(m, ctypes.c_uint64(len(m)), o)
+    load().nth_sha512(m, ctypes.c_uint64(len(m)), o, int(one_site))
     return o.raw
 
 

@@ -207,9 +207,10 @@ int nth_halfsize_disagree(const uint8_t* ks, int n) {
   }
   return bad;
 }
-void nth_sha512(const uint8_t* msg, uint64_t len, uint8_t* out64) {
+void nth_sha512(const uint8_t* msg, uint64_t len, uint8_t* out64, int one_site) {
   uint64_t st[8];
-  sha512_prefixed<0>(st, nullptr, msg, len);
+  if (one_site) sha512_prefixed_1site<0>(st, nullptr, msg, len);
+  else sha512_prefixed<0>(st, nullptr, msg, len);
   uint32_t w[16];
   sha512_out_words(w, st, 16);
   std::memcpy(out64, w, 64);

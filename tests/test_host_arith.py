@@ -89,10 +89,13 @@ def test_sc_reduce512():
 
 
 def test_sha512_host_build():
-    for n in (0, 1, 111, 112, 127, 128, 129, 255, 256, 1000, 5000):
+    """both block loops: sha512_prefixed and the one-compression-site form the
+    digest kernel uses (sha512_prefixed_1site), at every padding boundary"""
+    for n in (0, 1, 111, 112, 113, 127, 128, 129, 239, 240, 255, 256, 1000, 3336, 5000):
         m = bytes(range(256)) * (n // 256 + 1)
         m = m[:n]
         assert H.sha512(m) == hashlib.sha512(m).digest()
+        assert H.sha512(m, one_site=True) == hashlib.sha512(m).digest()
 
 
 def test_hram_one_block_path_matches_hashlib():
