@@ -16,8 +16,10 @@
 //     carries 2^510, removed by one multiply at the end).
 //   * at the end b = gcd(z, p) = 1 for z != 0 and v = z^-1 2^510; z = 0 gives 0
 //     (as z^(p-2) does).
-// Every lane runs the same fixed schedule (17 x 30 steps, selects instead of
-// branches), so lanes never diverge.  Numbers are 9 limbs of 30 bits; the
+// Every lane runs the same schedule (30 steps per iteration, selects instead of
+// branches), so lanes never diverge; the wave leaves the loop once a = 0 in all
+// of its lanes (13-14 iterations instead of 17) and applies the remaining
+// iterations' factor 2^30 each directly.  Numbers are 9 limbs of 30 bits; the
 // matrix application is one v_mad_i64_i32 per limb and entry.
 #pragma once
 #include "ge25519.hpp"
@@ -27,12 +29,26 @@ namespace nt {
 constexpr uint32_t kM30 = 0x3fffffffu;
 constexpr int kGcdOuter = 17;  // ceil((2 * 255 - 1) / 30)
 constexpr int kGcdInner = 30;  // k - 1
+// -DNT_GCD_EARLY_EXIT=0 (A/B): all 17 iterations in every wave
+#ifndef NT_GCD_EARLY_EXIT
+#define NT_GCD_EARLY_EXIT 1
+#endif
+constexpr bool kGcdEarlyExit = NT_GCD_EARLY_EXIT != 0;
 
 NT_HD NT_INLINE uint32_t clz32(uint32_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return (uint32_t)__clz((int)x);
 #else
   return x ? (uint32_t)__builtin_clz(x) : 32u;
+#endif
+}
+
+// any lane of the wave (the host build: this lane)
+NT_HD NT_INLINE bool gcd_wave_any(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ballot(x != 0) != 0;
+#else
+  return x != 0;
 #endif
 }
 
@@ -135,8 +151,15 @@ NT_HD NT_INLINE void fe_invert_vt(fe& out, const fe& z) {
     u[i] = i == 0 ? 1u : 0u;
     v[i] = 0u;
   }
+  int it = 0;
 #pragma unroll 1
-  for (int it = 0; it < kGcdOuter; ++it) {
+  for (; it < kGcdOuter; ++it) {
+    // a = 0 in every lane: nothing is left to reduce (a lane reaches it after 12-13
+    // of the 17 iterations, a wave of 64 after 13-14: tools/isa/gcd_iterations.py)
+    uint32_t anz = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) anz |= a[i];
+    if (kGcdEarlyExit && !gcd_wave_any(anz)) break;
     uint32_t ab[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) ab[i] = a[i] | b[i];
@@ -178,6 +201,15 @@ NT_HD NT_INLINE void fe_invert_vt(fe& out, const fe& z) {
       u[i] = nu[i];
       v[i] = nv[i];
     }
+  }
+  // An iteration with a = 0 leaves b = 1 and multiplies v by 2^30 (its matrix
+  // is f1 = 0, g1 = 2^30): the skipped ones, done directly, keep the 2^510 below
+#pragma unroll 1
+  for (; it < kGcdOuter; ++it) {
+    uint32_t nv[9];
+    gcd_lincomb_modp(nv, u, v, 0, 1 << 30);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) v[i] = nv[i];
   }
   // v = z^-1 2^510 mod p, v < 2^257: radix-2^25.5 limbs (limb 9 takes bits 230..256, < 2^27)
   fe vf;

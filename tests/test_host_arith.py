@@ -354,7 +354,9 @@ def _invert(limbs, vt):
 
 def test_fe_invert_vt_vs_fermat_and_bigint():
     """The key-cache kernel's variable-time inversion (fe_inv_vt.hpp: Pornin's
-    optimized binary GCD, 17 x 30 steps on 62-bit approximations) equals
+    optimized binary GCD, up to 17 x 30 steps on 62-bit approximations, leaving
+    the loop once a = 0 -- on the host per value, so small inputs exercise the
+    skipped iterations' direct factor 2^30) equals
     z^(p-2) mod p (Python big integers) on edge values and random inputs, and
     equals the Fermat chain (fe_invert) on 200k more inputs drawn in the C
     harness (half of them structured: small, p - small, powers of two, p + s
