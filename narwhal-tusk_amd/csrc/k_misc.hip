@@ -500,19 +500,6 @@ constexpr int kHistTile = 16;            // independent key loads in flight per 
 // 1,661 blocks, ~1.6 ns per atomic on one of 4 lines; k_key_hist 43 us whatever
 // the size, one dependent load + LDS atomic per loop iteration).
 constexpr uint32_t kCtrStride = 32;
-// LDS of the two sort kernels, sized to the committee (nkeys + 1 buckets) rather
-// than to kSortBuckets: at 16 / 33 KB per block they were not placed beside a
-// two-waves-per-SIMD key-cache launch of the other stream and waited for its
-// waves to exit (rocprofv3 trace r05as: k_key_scatter 720-750 us instead of ~15)
-// NT_SORT_LDS_FULL=1 (A/B): the round-4 sizes (kSortBuckets buckets whatever the committee)
-inline size_t sort_lds_bytes(uint32_t nkeys, bool scatter) {
-  static const bool full = [] {
-    const char* e = std::getenv("NT_SORT_LDS_FULL");
-    return e && *e == '1';
-  }();
-  const size_t nb = full ? kSortBuckets : nkeys + 1;
-  return ((scatter ? 2 : 1) * nb + (scatter ? kBlock : 0)) * 4;
-}
 
 NT_D NT_INLINE uint32_t sort_bucket(uint32_t k, int mixed, uint32_t nkeys) {
   if (mixed) k &= ~kKeyWantStrict;
@@ -522,7 +509,7 @@ NT_D NT_INLINE uint32_t sort_bucket(uint32_t k, int mixed, uint32_t nkeys) {
 __global__ __launch_bounds__(kBlock) void k_key_hist(const uint32_t* __restrict__ key, uint64_t n, int mixed,
                                                     uint32_t nkeys, uint32_t* __restrict__ hist) {
   aux_priority();
-  extern __shared__ uint32_t h[];  // nkeys + 1 buckets (sort_lds_bytes)
+  __shared__ uint32_t h[kSortBuckets];
   for (uint32_t b = threadIdx.x; b <= nkeys; b += kBlock) h[b] = 0;
   __syncthreads();
   const uint64_t stride = (uint64_t)gridDim.x * kBlock * kHistTile;
@@ -550,11 +537,10 @@ __global__ __launch_bounds__(kBlock) void k_key_scatter(const uint32_t* __restri
                                                        uint32_t nkeys, uint32_t* __restrict__ lines,
                                                        uint32_t* __restrict__ perm) {
   aux_priority();
+  __shared__ uint32_t cnt[kSortBuckets];
+  __shared__ uint32_t base[kSortBuckets];
+  __shared__ uint32_t part[kBlock];
   const uint32_t nb = nkeys + 1, per = (nb + kBlock - 1) / kBlock, b0 = threadIdx.x * per;
-  extern __shared__ uint32_t smem[];  // cnt[nb], base[nb], part[kBlock] (sort_lds_bytes)
-  uint32_t* cnt = smem;
-  uint32_t* base = smem + nb;
-  uint32_t* part = smem + 2 * nb;
   uint32_t sum = 0;
   for (uint32_t b = b0; b < b0 + per && b < nb; ++b) sum += lines[b * kCtrStride];
   part[threadIdx.x] = sum;
@@ -665,11 +651,9 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
       // LDS histogram with one global atomic per bucket)
       const uint64_t hw = (m + (uint64_t)kBlock * kHistTile - 1) / ((uint64_t)kBlock * kHistTile);
       const uint32_t hb = (uint32_t)(hw < 512 ? hw : 512);
-      hipLaunchKernelGGL(k_key_hist, dim3(hb), dim3(kBlock), sort_lds_bytes(nkeys, false), s, d_key_idx + lo, m, mixed,
-                         nkeys, hist);
+      hipLaunchKernelGGL(k_key_hist, dim3(hb), dim3(kBlock), 0, s, d_key_idx + lo, m, mixed, nkeys, hist);
       const uint64_t sb = (m + (uint64_t)kBlock * kSortTile - 1) / ((uint64_t)kBlock * kSortTile);
-      hipLaunchKernelGGL(k_key_scatter, dim3((uint32_t)sb), dim3(kBlock), sort_lds_bytes(nkeys, true), s, d_key_idx + lo,
-                         m, mixed, nkeys, hist,
+      hipLaunchKernelGGL(k_key_scatter, dim3((uint32_t)sb), dim3(kBlock), 0, s, d_key_idx + lo, m, mixed, nkeys, hist,
                          p);
       if ((e = hipGetLastError()) != hipSuccess) return e;
       perm = p;
