@@ -39,15 +39,14 @@ inline std::vector<uint64_t> verify_chunk_targets(uint64_t total, uint64_t R1, u
   return t;
 }
 
-// Item counts per chunk.  A host call is PCIe-bound (config 2: 608 B per
-// verify over a ~48 GB/s link against ~95 verifies per us of kernel), and its
-// copies run back to back on the copy stream, so the call takes about the whole
-// copy plus the kernels that can only start after the LAST copy.  So: a
-// quarter-round first chunk (the first kernel starts after a short copy), whole
-// rounds R in the middle (a launch fills the GPU), and a quarter-round last
-// chunk (the tail after the last copy is one short launch).  NT_PIPE_PLAN=round
-// restores round 4's plan (one-round first chunk, equal whole-round chunks, the
-// rest last) for A/B (round4).
+// Item counts per chunk (the key-cache, group and digest calls).  A host call's
+// copies run back to back on the copy stream, so it takes about the whole copy
+// plus the kernels that can only start after the LAST copy.  Calls of at least
+// two rounds R ramp at both ends (below); shorter ones take a quarter-round
+// first chunk (the first kernel starts after a short copy), whole rounds R in
+// the middle and at most a quarter round last.  NT_PIPE_PLAN=round restores
+// round 4's plan (one-round first chunk, equal whole-round chunks, the rest
+// last) for A/B (round4).
 inline std::vector<uint64_t> chunk_targets(uint64_t total, uint64_t R, uint64_t cap, bool round4 = false) {
   if (cap <= 1 || total <= R) return {total};
   if (!round4 && cap >= 6 && total >= 2 * R) {
