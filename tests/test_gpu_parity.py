@@ -81,11 +81,13 @@ def test_sha512_random_lengths_and_alignment(be):
 
 
 def test_sha512_both_kernels(be):
-    """n <= 32768 runs the two-wave producer/consumer kernel, larger n the
-    one-lane-per-message kernel: both against hashlib, with long and ragged
-    messages in the same call (lanes with different block counts)."""
+    """All three digest kernels against hashlib, with long and ragged messages
+    in the same call (lanes with different block counts): n <= 32768 with a
+    message of >= 16 KB runs the two-wave producer/consumer kernel (n = 1000),
+    other launches of <= 65,536 messages the 80-VGPR one-lane kernel (n = 3,
+    33000), larger ones the general one-lane kernel (n = 70000)."""
     rng = np.random.default_rng(7)
-    for n in (3, 1000, 33000):
+    for n in (3, 1000, 33000, 70000):
         lens = rng.integers(0, 300, n).astype(np.uint64)
         lens[: min(n, 5)] = [0, 111, 112, 128, 2000][: min(n, 5)]
         if n == 1000:
