@@ -1300,9 +1300,9 @@ def keyset_roofline(launch_ms, step_ms, nsig):
             "effective_clock_ghz": round(pk["effective_clock_ghz"], 3) if "effective_clock_ghz" in pk else None,
             "valu_issue_share": round(pk["valu_issue_share_4cyc"], 3) if "valu_issue_share_4cyc" in pk else None,
             "traffic": pk.get("hbm_bytes_per_launch"),
-            "traffic_note": "HBM bytes per launch (profiles/%s, FETCH_SIZE*2 + WRITE_SIZE): 24 random 128-B comb "
-                            "lines (3 KB) + ~250 B of inputs + the 160-B stash round trip per signature"
-                            % PMC_KEYSET_PROFILE}
+            "traffic_note": "HBM bytes per launch (profiles/%s, FETCH_SIZE*2 + WRITE_SIZE): 23 random 128-B comb "
+                            "lines (2.9 KB: 12 of the 21-bit key comb, 11 of the 24-bit comb of B) + ~250 B of "
+                            "inputs + the 160-B stash round trip per signature" % PMC_KEYSET_PROFILE}
 
 
 def bench_latency(be, pk_h, sig_h, msg_h, L):
