@@ -891,10 +891,15 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
     }
     const uint64_t sw = W[C], gw = (gm + 63) / 64;
     const uint64_t mm = std::max<uint64_t>(m, 1);
-    // caller's keys and signatures already in nt_host_alloc memory and densely
-    // packed: DMA straight from them, no staging copy
-    bool direct = m > 0 && is_pinned(keys + kw * first[glo], kw * m) && is_pinned(sig64 + 64 * first[glo], 64 * m);
+    // densely packed keys and signatures are copied straight from the caller's
+    // arrays: a DMA from nt_host_alloc memory, or HIP's own staged copy from
+    // pageable memory (which returns when it is done: run_chunks' staged order);
+    // scattered groups are gathered into the pinned staging on a helper thread
+    bool direct = m > 0;
     for (uint64_t g = glo; direct && g + 1 < ghi; ++g) direct = first[g + 1] == first[g] + cnt[g];
+    const bool direct_pinned =
+        direct && is_pinned(keys + kw * first[glo], kw * m) && is_pinned(sig64 + 64 * first[glo], 64 * m);
+    if (direct && !direct_pinned && std::getenv("NT_GROUPS_GATHER")) direct = false;  // A/B: round-5 staging
     NT_CHK(dv.h[B_PK].ensure(direct ? 1 : mm * kw));
     NT_CHK(dv.h[B_SIG].ensure(direct ? 1 : mm * 64));
     NT_CHK(dv.h[B_FIRST].ensure(gm * 8));
@@ -929,10 +934,11 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
     uint8_t* hmsg = dv.h[B_DATA].as<uint8_t>();
     hipStream_t cs = dv.cstream;
     NT_TRY(hipMemsetAsync(dv.d[B_OUT].p, 0, sw * 8 + 8, cs));  // before chunk 0's copy-done event
-    // direct: every copy is a DMA from pinned memory, so chunk c+1's copies are
-    // queued before the host waits on chunk c; staged: a helper thread stages
-    // (host memcpy of keys and signatures) and issues the chunks ahead of the
-    // launches (run_chunks_staged)
+    // direct from pinned memory: every copy is a DMA, so chunk c+1's copies are
+    // queued before the host waits on chunk c; direct from pageable memory: chunk
+    // c's kernels are launched before chunk c+1's (synchronous) copies; gathered:
+    // a helper thread stages (host memcpy of keys and signatures) and issues the
+    // chunks ahead of the launches (run_chunks_staged)
     auto copy = [&](size_t c) -> int {
       const uint64_t g0 = ch[c].first, g1 = ch[c].second, gl = g0 - glo, e0 = E[c], mc = E[c + 1] - E[c];
       // chunk-local: hfirst relative to e0; message offsets 32 * (g - g0) made on the device
@@ -983,7 +989,8 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
                                   dv.d[B_OUT2].as<uint64_t>() + gl / 64, s));
       return NT_OK;
     };
-    NT_CHK(direct || m == 0 ? run_chunks(dv, C, true, copy, launch) : run_chunks_staged(dv, C, copy, launch));
+    NT_CHK(direct || m == 0 ? run_chunks(dv, C, direct_pinned || m == 0, copy, launch)
+                            : run_chunks_staged(dv, C, copy, launch));
     hipStream_t s = dv.stream;
     NT_CHK(finish_chunks(dv));
     NT_TRY(hipMemcpyAsync(dv.h[B_OUT2].p, dv.d[B_OUT2].p, gw * 8, hipMemcpyDeviceToHost, s));
