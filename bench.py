@@ -189,6 +189,29 @@ class Region:
         return max(self.ev0.elapsed_time(e) for e in self.ends)
 
 
+class ClockProbe:
+    """The run's own clock: nt_dev_clock_probe -- the verify
+    kernels' mix of v_mad_u64_u32 and 64-bit carry adds on every SIMD at two
+    waves per SIMD for ~2.5 ms, each wave stamping the shader-clock and the
+    100 MHz wall-clock counters -- run right before and right after a timed
+    region on the region's stream.  The chip holds a clock that depends on the
+    load (MI355X_MICROARCH.md "DVFS give-back"), so this is the box's clock
+    under a verify-like integer load, measured in the same process; the timed
+    kernels' own clock relates to it by the ratio DESIGN.md §9 records from a
+    same-box PMC profile."""
+    ITERS = 8192
+
+    def __init__(self, torch, be, dev):
+        self.torch, self.be = torch, be
+        self.buf = torch.zeros(2, dtype=torch.int64, device=dev)
+
+    def ghz(self, stream):
+        khz = self.be.dev_clock_probe(0, stream.cuda_stream, self.ITERS, self.buf.data_ptr())
+        stream.synchronize()
+        cyc, wall = (int(x) for x in self.buf.cpu())
+        return cyc / max(wall, 1) * khz / 1e6
+
+
 def side_streams(torch, dev, n):
     """Streams for the header-id digests of the pipelined config-3 steps (one per
     pipeline slot, the highest priority: HIP keeps a queue pool per priority,
@@ -358,8 +381,10 @@ def main():
             lev[-1][1].record(st)
 
     barrier()  # the inputs were written on `stream`; the library's streams are ordered against no other
+    probe = ClockProbe(torch, be, dev)
     for i in range(args.warmup):
         step(i)
+    clk_before = probe.ghz(streams[0])  # after the warm-up launches: the clock under load
     barrier()
     t0 = time.perf_counter()
     reg.start()
@@ -368,6 +393,7 @@ def main():
     reg.end()
     barrier()
     wall = time.perf_counter() - t0
+    clk_after = probe.ghz(streams[0])
     step_ms = reg.ms() / args.steps          # per batch, steady state
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in lev]))  # per launch
     ranks_cfg2 = nd.gather_object({"rank": rank, "device": local, "signatures": n, "kernel_ms": round(kernel_ms, 3),
@@ -420,7 +446,28 @@ def main():
                               "dispatch's duration (MI355X_MICROARCH.md, DVFS give-back); frac_at_effective_clock "
                               "prices the mad peak at that clock instead of 2.4 GHz",
                 "issue_note": "the kernel is VALU-issue-bound (issue share from the PMC profile); non-mad VALU work "
-                              "(carries, pre-scaling, SHA-512, lattice reduction) is why mad frac < issue share"}
+                              "(carries, pre-scaling, SHA-512, lattice reduction) is why mad frac < issue share",
+                "pmc_source": "traffic, valu_instr_per_verify, valu_issue_share and effective_clock_ghz come from "
+                              "profiles/%s (a separate rocprofv3 --pmc run of the same build, on another box); "
+                              "run_clock is this run's own" % PMC_PROFILE}
+    run_ghz = (clk_before + clk_after) / 2
+    roofline["run_clock"] = {"probe_ghz_before": round(clk_before, 3), "probe_ghz_after": round(clk_after, 3),
+                             "probe_ghz": round(run_ghz, 3),
+                             "note": "nt_dev_clock_probe right before and right after the one-stream timed region on "
+                                     "its stream (ClockProbe): the shader clock this box holds under a verify-like "
+                                     "v_mad_u64_u32 load in this run"}
+    roofline["frac_at_run_clock"] = round(achieved / (MAD_PEAK_TS * run_ghz / 2.4), 4)
+    roofline["kernel_mcycles_at_run_clock"] = round(kernel_ms * run_ghz * 1e3, 1)
+    # round 5's driver run: 11.308 ms per 1M launch (BENCH_r05.json); its clock was not measured
+    # in that run -- the r05b PMC profile's effective clock of the same launch (another box) stands in
+    r05 = {"kernel_ms": 11.308, "clock_ghz": 1.979}
+    roofline["vs_r05"] = {"kernel_ms_r05": r05["kernel_ms"], "kernel_ms": round(kernel_ms, 3),
+                          "time_ratio_r05_over_now": round(r05["kernel_ms"] / kernel_ms, 4),
+                          "clock_r05_ghz": r05["clock_ghz"], "clock_now_ghz": round(run_ghz, 3),
+                          "cycle_ratio_r05_over_now": round(r05["kernel_ms"] * r05["clock_ghz"] / (kernel_ms * run_ghz), 4),
+                          "note": "time_ratio > 1: this run's launch is faster; cycle_ratio normalises both by their "
+                                  "clock (r05: the PMC effective clock of its profile, no run clock existed; now: "
+                                  "the run's probe) -- ~1 means the same instruction stream at a different clock"}
 
     # the other two halves of the metric, filled in when their configs have run, so
     # that they sit near the front of the line (a reader of its first few hundred
@@ -589,9 +636,9 @@ def cfg2_two_streams(torch, be, dev, stream, ntcrypto, pk, sig, msgs, off, ln, n
     return {"verifies_per_s": round(n * world * args.steps / wall, 1), "ms_per_step": round(wall * 1e3 / args.steps, 3),
             "gpu_ms_per_step": round(reg.ms() / args.steps, 3),
             "mismatches_vs_expected": int(max_over_ranks(mism)),
-            "note": "consecutive 1M batches alternating between two streams on different hardware queues; "
-                    "the headline `value` is one stream, "
-                    "launches strictly back to back"}
+            "note": "consecutive 1M batches alternating between two streams on different hardware queues: the "
+                    "headline `value` (NT_BENCH_HEADLINE=one makes it the one-stream rate, launches strictly back "
+                    "to back, which `one_stream` reports beside it)"}
 
 
 def bench_sha(args, torch, dev, be, sp, stream, world, rank, barrier, max_over_ranks):
@@ -928,6 +975,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
         perm = perm.cpu().numpy()
 
     kev = []  # (start, end) events around the key-cache launch of each timed step
+    probe = ClockProbe(torch, be, dev)
 
     mode_streams = {True: nst, False: 1}  # streams of the cached / uncached runs
 
@@ -1009,6 +1057,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
         barrier()
         for i in range(max(1, args.warmup)):
             step(cached, i)
+        clk = [probe.ghz(streams[0])] if key == "keyset" else []
         barrier()
         reg = Region(torch, streams[:slots(cached)] + (side if side and slots(cached) > 1 else []), stream)
         t0 = time.perf_counter()
@@ -1018,6 +1067,8 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
         reg.end()
         barrier()
         wall_r = time.perf_counter() - t0
+        if clk:
+            clk.append(probe.ghz(streams[0]))
         wall = max_over_ranks(wall_r)
         kms = reg.ms() / steps
         if key == "keyset":
@@ -1031,7 +1082,7 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                     "ms_per_step": round(wall * 1e3 / steps, 3), "gpu_ms_per_step": round(kms, 3),
                     "streams": slots(cached), "mismatches_vs_expected": mism}
         if key == "keyset" and fused and kev:
-            out[key]["roofline"] = keyset_roofline(np.mean([a.elapsed_time(b) for a, b in kev]), kms, V + G)
+            out[key]["roofline"] = keyset_roofline(np.mean([a.elapsed_time(b) for a, b in kev]), kms, V + G, clk)
         if key == "keyset_one_stream" and kev and "keyset" in out and out["keyset"].get("roofline"):
             # launches strictly back to back: each one's own duration (sort + key-cache kernel +
             # byte pack, what rocprof sums per step) without the two-stream overlap
@@ -1114,6 +1165,14 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                 expect, out["keyset"]["certs_per_s"])
             progress("cfg3 shards A/B")
     ks.close()
+    # -------- the drop-in path: the same votes through nt_ed25519_verify_batch_groups
+    # (what the unchanged crate's Signature::verify_batch binds) with raw 32-byte keys,
+    # the committee keys in the context's key registry (nt_set_key_cache)
+    if os.environ.get("NT_BENCH_HOST_CERTS", "1") != "0":
+        out["host_api_plain"] = bench_cert_registry(be, pks, vpk, vsig, cdig, G, quorum, expect, barrier,
+                                                    max_over_ranks, world, G_total)
+        progress("cfg3 plain entry point + key registry: %.2f M certificates/s"
+                 % (out["host_api_plain"]["certs_per_s"] / 1e6))
     if world == 1 and not getattr(args, "no_cpu", False):
         out["cpu_baseline"] = cert_cpu_baseline(args, hdr, hlen, ids, tmp_pk, hsig, cpre, vpk, vsig, quorum, expect)
     out["_ranks"] = nd.rank_summary(ranks3)
@@ -1170,6 +1229,59 @@ def bench_cert_host_api(be, ks, vkey, vsig, cdig, G, quorum, expect, barrier, ma
             "note": "nt_ed25519_verify_batch_groups_keyset on %d certificates x %d votes per rank from nt_host_alloc "
                     "buffers (4-B key index + 64-B signature per vote over PCIe, no staging copy of them), the library's "
                     "chunk pipeline on its own streams; PCIe-inclusive, never `value`" % (G, quorum)}
+
+
+def bench_cert_registry(be, pks, vpk, vsig, cdig, G, quorum, expect, barrier, max_over_ranks, world, G_total,
+                        reps=3):
+    """Config 3's votes through the PLAIN entry point nt_ed25519_verify_batch_groups
+    (crypto/src/lib.rs:206-219, what INTEGRATION.md's unchanged verify_batch binds):
+    raw 32-byte keys, no key-set handle.  The context's key registry holds the
+    100 committee keys (nt_key_cache_add once, timed apart as a one-time cost --
+    the same tables a first sighting builds in the background); every call looks
+    each key up on host threads as its chunks are staged and sends 4-byte
+    indices over PCIe (68 B per vote).  From nt_host_alloc (pinned) buffers and
+    from ordinary numpy (pageable) arrays; PCIe-inclusive, never `value`."""
+    t0 = time.perf_counter()
+    be.set_key_cache(len(pks))   # the committee (config/src/lib.rs:140-143): its n keys
+    be.key_cache_add(pks)
+    build_s = time.perf_counter() - t0
+    info = be.key_cache_info()
+    vpk_h = vpk.cpu().numpy()
+    vsig_h = vsig.cpu().numpy()
+    msg32 = cdig.cpu().numpy()
+    first = np.arange(G, dtype=np.uint64) * quorum
+    cnt = np.full(G, quorum, np.uint32)
+    res = {}
+    for kind in ("pinned", "pageable"):
+        if kind == "pinned":
+            pk_a, sig_a = be.pinned((G * quorum, 32)), be.pinned((G * quorum, 64))
+            pk_a[...] = vpk_h
+            sig_a[...] = vsig_h
+        else:
+            pk_a, sig_a = vpk_h, vsig_h
+        got = be.verify_batch_groups(pk_a, sig_a, first, cnt, msg32)   # warm-up (staging, stash)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            got = be.verify_batch_groups(pk_a, sig_a, first, cnt, msg32)
+        barrier()
+        wall = max_over_ranks((time.perf_counter() - t0) / reps)
+        res[kind] = {"certs_per_s": round(G_total / wall, 1), "ms_per_call": round(wall * 1e3, 3),
+                     "mismatches_vs_expected": int(max_over_ranks(int((got != expect).sum())))}
+        del pk_a, sig_a
+    after = be.key_cache_info()
+    be.set_key_cache(0)
+    return {"certs_per_s": res["pinned"]["certs_per_s"], "ms_per_call": res["pinned"]["ms_per_call"],
+            "mismatches_vs_expected": res["pinned"]["mismatches_vs_expected"], "pageable": res["pageable"],
+            "sig_verifies_per_s": round(G_total * quorum / (res["pinned"]["ms_per_call"] * 1e-3), 1),
+            "key_registry": {"keys": info["keys"], "comb_bits": info["comb_bits"],
+                             "gb_per_device": round(info["bytes_per_device"] / 1e9, 2), "build_s": round(build_s, 3),
+                             "lookups_hit": after["hits"], "lookups_missed": after["misses"]},
+            "note": "nt_ed25519_verify_batch_groups (the plain entry point the crate's verify_batch binds) on %d "
+                    "certificates x %d votes per rank, raw 32-byte keys looked up in the context's key registry on "
+                    "host threads while the chunks are staged (4-B index + 64-B signature per vote over PCIe); "
+                    "pinned: keys and signatures in nt_host_alloc memory; pageable: ordinary numpy arrays; "
+                    "PCIe-inclusive, never `value`" % (G, quorum)}
 
 
 def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream, barrier, G,
@@ -1270,7 +1382,7 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream,
     return res
 
 
-def keyset_roofline(launch_ms, step_ms, nsig):
+def keyset_roofline(launch_ms, step_ms, nsig, clk=None):
     """The config-3 key-cache launch (k_ed25519_verify_keyset, NT_MODE_MIXED) against
     the same v_mad_u64_u32 issue peak as the headline kernel; the instruction
     count, issue share and HBM traffic come from the committed PMC profile.
@@ -1302,7 +1414,13 @@ def keyset_roofline(launch_ms, step_ms, nsig):
             "traffic": pk.get("hbm_bytes_per_launch"),
             "traffic_note": "HBM bytes per launch (profiles/%s, FETCH_SIZE*2 + WRITE_SIZE): 23 random 128-B comb "
                             "lines (2.9 KB: 12 of the 21-bit key comb, 11 of the 24-bit comb of B) + ~250 B of "
-                            "inputs + the 160-B stash round trip per signature" % PMC_KEYSET_PROFILE}
+                            "inputs + the 160-B stash round trip per signature" % PMC_KEYSET_PROFILE,
+            "pmc_source": "traffic, valu_instr_per_signature, valu_issue_share and effective_clock_ghz come from "
+                          "profiles/%s (a separate rocprofv3 --pmc run, another box); run_clock is this run's own"
+                          % PMC_KEYSET_PROFILE,
+            **({"run_clock": {"probe_ghz_before": round(clk[0], 3), "probe_ghz_after": round(clk[1], 3),
+                              "probe_ghz": round(sum(clk) / 2, 3)},
+                "frac_at_run_clock": round(achieved / (MAD_PEAK_TS * sum(clk) / 2 / 2.4), 4)} if clk else {})}
 
 
 def bench_latency(be, pk_h, sig_h, msg_h, L):
@@ -1326,24 +1444,51 @@ def bench_latency(be, pk_h, sig_h, msg_h, L):
         "verify_strict_n1": (lambda: be.verify_strict(*one), 200),
         "verify_batch_1x67": (lambda: be.verify_batch_groups(pk67, sig67, first, cnt, d), 100),
         "sha512_one_508052B": (lambda: be.digest_many(big), 30),
+        # the same lone calls through the PLAIN entry points with their keys in the
+        # context's key registry (nt_set_key_cache): the key-cache kernel's floor
+        "verify_strict_n1_key_cache": (lambda: be.verify_strict(*one), 200),
+        "verify_batch_1x67_key_cache": (lambda: be.verify_batch_groups(pk67, sig67, first, cnt, d), 100),
     }
     out = {"note": "per-call wall time (us) through the Python binding; gpu = small-call path off, "
-                   "auto = NT_SMALL_AUTO (calls below the crossover on host threads)"}
+                   "auto = NT_SMALL_AUTO (calls below the crossover on host threads); *_key_cache: the same calls "
+                   "with the 67 keys in the context's key registry (16-bit key combs: a lone call's floor is the "
+                   "launch and one lane's chain, 27 vs 23 comb additions at 21 bits)"}
+
+    def crossover(m, floor):
+        T = m["threads"]
+        nv = 0
+        while nv < 100000:
+            t = min(T, nv + 1)
+            if -(-(nv + 1) // t) * m["cpu_verify_us"] + (m["spawn_us"] if t > 1 else 0) >= m[floor]:
+                break
+            nv += 1
+        return nv
+
+    def registry(on):
+        if on:
+            saved = os.environ.get("NT_KEYSET_COMB_BITS")
+            os.environ["NT_KEYSET_COMB_BITS"] = "16"
+            be.set_key_cache(128)
+            be.key_cache_add(pk67)
+            if saved is None:
+                del os.environ["NT_KEYSET_COMB_BITS"]
+            else:
+                os.environ["NT_KEYSET_COMB_BITS"] = saved
+        else:
+            be.set_key_cache(0)
+
     for mode, name in ((ntcrypto.NT_SMALL_OFF, "gpu"), (ntcrypto.NT_SMALL_AUTO, "auto")):
         be.set_small_call_path(mode, 0)
         if mode == ntcrypto.NT_SMALL_AUTO:
             # the cost model AUTO routes by, calibrated on this context by the call above
             m = be.small_call_model()
-            T = m["threads"]
-            nv = 0
-            while nv < 100000:
-                t = min(T, nv + 1)
-                if -(-(nv + 1) // t) * m["cpu_verify_us"] + (m["spawn_us"] if t > 1 else 0) >= m["gpu_verify_us"]:
-                    break
-                nv += 1
             out["small_call_model"] = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in m.items()}
-            out["small_call_model"]["verify_crossover_signatures"] = nv
+            out["small_call_model"]["verify_crossover_signatures"] = crossover(m, "gpu_verify_us")
+            out["small_call_model"]["verify_crossover_signatures_key_cache"] = crossover(m, "gpu_keyset_us")
         for case, (fn, reps) in cases.items():
+            cached = case.endswith("_key_cache")
+            if cached:
+                registry(True)
             h0, g0 = be.call_counts()
             fn()
             ts = []
@@ -1356,6 +1501,11 @@ def bench_latency(be, pk_h, sig_h, msg_h, L):
             out.setdefault(case, {})[name] = {"p50_us": round(ts[len(ts) // 2], 1),
                                               "p99_us": round(ts[min(len(ts) - 1, int(len(ts) * 0.99))], 1),
                                               "reps": reps, "host_calls": h1 - h0, "gpu_calls": g1 - g0}
+            if cached:
+                ki = be.key_cache_info()
+                out[case][name]["key_cache"] = {"keys": ki["keys"], "comb_bits": ki["comb_bits"], "hits": ki["hits"],
+                                                "misses": ki["misses"]}
+                registry(False)
     # host-lane throughput of one thread (the small-call cost model's constants)
     be.set_small_call_path(ntcrypto.NT_SMALL_ALWAYS, 1)
     n = 64

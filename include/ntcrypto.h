@@ -93,8 +93,9 @@ const char *nt_version(void);
  * the widest that fits: 24-bit digits (11 additions per [s]B, 11.8 GB) when
  * the context's budget allows it and the device keeps 4 GB free beside it,
  * else 20-bit digits (13 additions, 872 MB); NT_BCOMB_BITS=24|20 forces one.
- * A key set (nt_keyset_create) reserves its key combs against the same budget
- * after the comb of B: 20 / 18 / 16-bit digits, the widest that fits.
+ * A key set (nt_keyset_create) or the key registry (nt_set_key_cache) reserves
+ * its key combs against the same budget after the comb of B: 21 / 20 / 18 /
+ * 16-bit digits, the widest that fits.
  *
  * nt_set_hbm_budget: bytes of such TABLES (comb of B + key combs) the context
  * may hold per device entry; 0 = no cap (the device's free memory decides).
@@ -160,7 +161,7 @@ int nt_keyset_create(nt_ctx *ctx, const uint8_t *pk32, uint32_t nkeys, nt_keyset
 void nt_keyset_free(nt_keyset *ks);
 /* flags of key i: bit 0 = decodes, bit 1 = small order */
 int nt_keyset_flags(const nt_keyset *ks, uint32_t i, uint32_t *flags);
-/* comb digit width of the set (16, 18 or 20) and its device bytes per device */
+/* comb digit width of the set (16, 18, 20 or 21) and its device bytes per device */
 int nt_keyset_info(const nt_keyset *ks, uint32_t *comb_bits, uint64_t *bytes_per_device);
 int nt_ed25519_verify_keyset(nt_ctx *ctx, const nt_keyset *ks, int mode, const uint32_t *key_idx,
                              const uint8_t *sig64, const uint8_t *msg, const uint64_t *off,
@@ -169,6 +170,41 @@ int nt_ed25519_verify_batch_groups_keyset(nt_ctx *ctx, const nt_keyset *ks, cons
                                           const uint8_t *sig64, const uint64_t *first,
                                           const uint32_t *cnt, const uint8_t *msg32, uint64_t G,
                                           uint8_t *out_group_bitmap, uint8_t *out_sig_bitmap);
+
+/* ---- key registry: the committee key cache behind the plain entry points --
+ * The reference's crate binds Signature::verify / verify_batch with raw
+ * PublicKeys (crypto/src/lib.rs:200-219): no committee handle crosses it.  With
+ * a registry enabled, nt_ed25519_verify_strict and
+ * nt_ed25519_verify_batch_groups look every 32-byte key up in it (a host-side
+ * index, before the keys cross PCIe: a registered key travels as a 4-byte
+ * index); registered keys verify through the key-cache kernel, the others
+ * through the uncached kernel in the same call, same verdicts either way.  A
+ * key that misses is counted, and after `admit_after` sightings (>= 1) a
+ * background thread builds its key combs on every device entry (on a
+ * low-priority stream of its own) and publishes it: later calls find it.
+ * Every key the reference passes to these calls is a committee member
+ * (primary/src/messages.rs:86-100, 155-163, 189-215) and the committee is
+ * static (config/src/lib.rs:140-143), so the registry holds at most max_keys
+ * keys and never evicts; keys that do not decode are never admitted (they
+ * reject either way).  Its comb width is chosen at the first admission for
+ * max_keys keys, as for a key set (21 / 20 / 18 / 16 bits, against the
+ * context's HBM budget); its tables are allocated then, not before.
+ *
+ * nt_set_key_cache: max_keys in [1, NT_KEY_CACHE_MAX], 0 = off (the default;
+ * NT_KEY_CACHE=<max_keys>[:<admit_after>] in the environment at nt_init sets
+ * it).  Call it before the context's verify calls, not concurrently with them.
+ * nt_key_cache_add: admit these keys now (waits for their tables).
+ * nt_key_cache_sync: wait until every queued admission is published; returns
+ * the registry's error (NT_ENOMEM: its tables did not fit, it admits no more).
+ * nt_key_cache_info out10: keys, max_keys, comb bits, device bytes per device
+ * entry (0 before the first admission), lookups that hit, lookups that missed,
+ * keys admitted, keys refused (do not decode / tables failed), admissions
+ * pending, -error. */
+#define NT_KEY_CACHE_MAX 4095u
+int nt_set_key_cache(nt_ctx *ctx, uint32_t max_keys, uint32_t admit_after);
+int nt_key_cache_add(nt_ctx *ctx, const uint8_t *pk32, uint32_t n);
+int nt_key_cache_sync(nt_ctx *ctx);
+int nt_key_cache_info(const nt_ctx *ctx, uint64_t *out10);
 
 /* ---- certificate ingestion from wire bytes --------------
  * The primary's receiver deserializes every PrimaryMessage with bincode
@@ -239,13 +275,17 @@ int nt_call_counts(const nt_ctx *ctx, uint64_t *host_calls, uint64_t *gpu_calls)
  * and SHA-512 rate on one thread, the pool wake-up on `threads` threads, and
  * the GPU floors from real calls (a one-signature verify, a 64-byte and a
  * 1 MiB digest); NT_SMALL_* environment variables override single fields.
- * out9 = cpu_verify_us, gpu_verify_us, cpu_sha_mbs, gpu_lane_mbs, gpu_call_us,
- * pcie_gbs, spawn_us, threads, calibrated (0/1).  A verify call of n signatures
- * runs on the host iff ceil(n / T) * cpu_verify_us + (T > 1 ? spawn_us : 0) <
- * gpu_verify_us (T = min(threads, n)); a digest call iff max(longest, total /
- * T) / cpu_sha_mbs + (T > 1 ? spawn_us : 0) < gpu_call_us + longest /
- * gpu_lane_mbs + total / (1000 pcie_gbs) (bytes, microseconds). */
-int nt_small_call_model(const nt_ctx *ctx, double *out9);
+ * out10 = cpu_verify_us, gpu_verify_us, cpu_sha_mbs, gpu_lane_mbs, gpu_call_us,
+ * pcie_gbs, spawn_us, threads, calibrated (0/1), gpu_keyset_us.  A verify call
+ * of n signatures runs on the host iff ceil(n / T) * cpu_verify_us + (T > 1 ?
+ * spawn_us : 0) < the GPU floor of the kernel it would run (T = min(threads,
+ * n)): gpu_keyset_us (a one-signature call through the key-cache kernel, timed
+ * on a one-key 16-bit key set) for key-set calls and registry calls whose keys
+ * all hit, gpu_verify_us (the uncached kernel) otherwise; a digest call iff
+ * max(longest, total / T) / cpu_sha_mbs + (T > 1 ? spawn_us : 0) < gpu_call_us
+ * + longest / gpu_lane_mbs + total / (1000 pcie_gbs) (bytes, microseconds;
+ * csrc/small_model.hpp). */
+int nt_small_call_model(const nt_ctx *ctx, double *out10);
 
 /* ---- pinned host buffers ---------------------------------------------
  * Page-locked host memory for callers that stage large batches themselves
@@ -308,6 +348,16 @@ int nt_dev_ed25519_verify_keyset(nt_ctx *ctx, const nt_keyset *ks, int dev, void
                                  const uint32_t *d_key_idx, const uint8_t *d_sig64, const uint8_t *d_msg,
                                  uint64_t msg_bytes, const uint64_t *d_off, const uint64_t *d_len, uint64_t n,
                                  uint64_t *d_out_words);
+/* Diagnostics (no reference counterpart): the shader clock of device entry
+ * `dev` under a fixed integer-multiply load enqueued on `stream` -- every CU
+ * runs `iters` x 64 dependent-pair v_mad_u64_u32 per lane for ~1-2 ms while
+ * each wave reads the shader-clock and the constant-rate wall-clock counters at
+ * its start and end.  out2 (device memory, 2 x uint64, written by the kernel):
+ * summed shader-clock cycles and summed wall-clock ticks over the waves; their
+ * ratio x the wall clock's rate (*wall_khz) is the effective clock.  bench.py
+ * brackets its timed regions with it. */
+int nt_dev_clock_probe(nt_ctx *ctx, int dev, void *stream, uint32_t iters, uint64_t *d_out2, uint64_t *wall_khz);
+
 /* d_sig64 may be NULL (keygen only; d_msg, d_off, d_len ignored). */
 int nt_dev_ed25519_sign(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_seed32, const uint8_t *d_msg,
                         uint64_t msg_bytes, const uint64_t *d_off, const uint64_t *d_len, uint64_t n,

@@ -199,6 +199,13 @@ void sha512_trunc32(const uint8_t* msg, uint64_t len, uint8_t out32[32]) {
   std::memcpy(out32, w, 32);
 }
 
+bool key_decodes(const uint8_t pk32[32]) {
+  uint32_t w[8];
+  std::memcpy(w, pk32, 32);
+  ge_p3 P;
+  return ge_frombytes_w(P, w) != 0;
+}
+
 bool verify(int mode, const uint8_t pk32[32], const uint8_t sig64[64], const uint8_t* msg, uint64_t len) {
   uint32_t A[8], R[8], S[8];
   std::memcpy(A, pk32, 32);

@@ -36,6 +36,10 @@ void sha512_trunc32(const uint8_t* msg, uint64_t len, uint8_t out32[32]);
 // verify_batch under SURVEY A.3).  Requires init().
 bool verify(int mode, const uint8_t pk32[32], const uint8_t sig64[64], const uint8_t* msg, uint64_t len);
 
+// the 32-byte encoding decodes to a curve point (ge_frombytes_w, as the
+// device's key tables decide it; the key registry admits only such keys)
+bool key_decodes(const uint8_t pk32[32]);
+
 // threads the worker pool runs with the caller (min(64, hardware threads)): the
 // most parallelism a host-lane call gets
 int pool_threads();

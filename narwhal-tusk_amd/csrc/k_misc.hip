@@ -16,6 +16,7 @@
 //   k_ed25519_sign        keygen + RFC 8032 signing (corpus generation / SignatureService
 //                         batch form; crypto/src/lib.rs:163-191) -- not constant time
 //   k_wcomb_bases/fill    wide-comb construction (B once per device, committee keys)
+//   k_clock_probe         diagnostics: the shader clock under a fixed multiply load (bench.py)
 //
 // SIMT design: every lane runs the same window schedule (fixed signed windows,
 // a wave-uniform window count, never per-lane sliding windows), so lanes of a
@@ -344,6 +345,58 @@ __global__ __launch_bounds__(kBlock) void k_ed25519_sign(const uint32_t* __restr
       }
     }
   }
+}
+
+// --------------------------------------------------------------------------
+// Clock probe (nt_dev_clock_probe): the verify kernels' instruction mix --
+// v_mad_u64_u32 partial products with 64-bit carry shifts and adds -- on every
+// SIMD at two waves per SIMD for `iters` x 16 steps of 4 independent chains;
+// each wave stamps the shader-clock counter (one tick per shader cycle) and the
+// 100 MHz wall-clock counter around its loop and adds the differences to out[0]
+// / out[1] (zeroed by the launcher).  Their ratio is the clock the chip holds
+// under this load (MI355X_MICROARCH.md "DVFS give-back" item 6).
+// --------------------------------------------------------------------------
+NT_D NT_INLINE uint64_t stamp_cycles() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+NT_D NT_INLINE uint64_t stamp_wall() {
+  uint64_t t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+__global__ __launch_bounds__(kBlock, 2) void k_clock_probe(uint32_t iters, uint32_t seed,
+                                                          unsigned long long* __restrict__ out) {
+  const uint32_t x0 = seed ^ (threadIdx.x * 0x9e3779b9u), x1 = x0 * 3u + 1u, x2 = x0 * 5u + 7u, x3 = x0 * 9u + 3u;
+  uint64_t a0 = x0, a1 = x1, a2 = x2, a3 = x3;
+  const uint64_t c0 = stamp_cycles(), w0 = stamp_wall();
+#pragma unroll 1
+  for (uint32_t i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      a0 = (uint64_t)(uint32_t)a0 * x1 + (a0 >> 26);
+      a1 = (uint64_t)(uint32_t)a1 * x2 + (a1 >> 26);
+      a2 = (uint64_t)(uint32_t)a2 * x3 + (a2 >> 26);
+      a3 = (uint64_t)(uint32_t)a3 * x0 + (a3 >> 26);
+    }
+  }
+  const uint64_t c1 = stamp_cycles(), w1 = stamp_wall();
+  if ((threadIdx.x & 63u) == 0) {
+    atomicAdd(&out[0], (unsigned long long)(c1 - c0));
+    atomicAdd(&out[1], (unsigned long long)(w1 - w0));
+  }
+  if ((a0 ^ a1 ^ a2 ^ a3) == 0x5a5a5a5a5a5a5a5aull) atomicAdd(&out[0], 1ull);  // keeps the chains live
+}
+
+hipError_t launch_clock_probe(uint32_t iters, uint32_t cus, uint64_t* d_out2, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(d_out2, 0, 16, s);
+  if (e != hipSuccess) return e;
+  const uint32_t blocks = cus * 4 * 2 * 64 / kBlock;  // two waves per SIMD
+  hipLaunchKernelGGL(k_clock_probe, dim3(blocks ? blocks : 1), dim3(kBlock), 0, s, iters, 0x2545f491u,
+                     (unsigned long long*)d_out2);
+  return hipGetLastError();
 }
 
 // --------------------------------------------------------------------------

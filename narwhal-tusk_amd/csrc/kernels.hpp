@@ -61,6 +61,8 @@ size_t wcomb_fill_tmp_bytes_per_key(int bits);
 uint32_t wcomb_fill_batch(int bits);  // keys per k_wcomb_fill launch
 size_t ws_bytes_per_slot();
 int verify_occupancy();  // waves per SIMD of the selected verify kernel variant
+// diagnostics: d_out2[0] / d_out2[1] = summed shader-clock cycles / 100 MHz ticks of a fixed multiply load
+hipError_t launch_clock_probe(uint32_t iters, uint32_t cus, uint64_t* d_out2, hipStream_t s);
 
 // ---- certificate ingestion on the device (k_ingest.hip, ingest_gpu.cpp) ----
 // Committee tables of an nt_committee on one device.

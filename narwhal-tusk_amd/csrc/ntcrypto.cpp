@@ -140,6 +140,40 @@ int verify_tables(Device& dv) {
   return dv.ensure_ws();
 }
 
+// Comb width of a new key set: the widest of 21 (reduced scalars) / 20 / 18 /
+// 16-bit digits (12 / 13 / 15 / 16 additions per [k]A; 1.61 GB / 872 / 252 /
+// 67 MB per key) that, on every device entry of the context, fits the
+// context's HBM budget beside the comb of B and the tables the entry already
+// holds, and leaves 1/8 of the device's HBM free.  With no width passing the
+// free-memory test the 16-bit combs are tried anyway (hipMalloc decides); 0 =
+// not even those fit the budget.  NT_KEYSET_COMB_BITS=16|18|20|21 forces one.
+int keyset_comb_bits(nt_ctx* ctx, uint32_t nkeys) {
+  if (const char* e = std::getenv("NT_KEYSET_COMB_BITS")) {
+    const int b = std::atoi(e);
+    if (b == nt::kKeyCombReduced || b == nt::kKeyCombWide || b == nt::kKeyCombMid || b == nt::kKeyCombNarrow)
+      return b;
+  }
+  const uint64_t nk = std::max<uint32_t>(nkeys, 1);
+  for (const int w : {nt::kKeyCombReduced, nt::kKeyCombWide, nt::kKeyCombMid, nt::kKeyCombNarrow}) {
+    const uint64_t comb = nt::wcomb_bytes_per_key(w) * nk;
+    const uint64_t need = comb + nt::wcomb_fill_tmp_bytes_per_key(w) * nt::wcomb_fill_batch(w);
+    bool ok = true;
+    for (auto& d : ctx->devs) {
+      size_t fr = 0, tot = 0;
+      if (!d->budget->fits(comb) || hipSetDevice(d->ordinal) != hipSuccess ||
+          hipMemGetInfo(&fr, &tot) != hipSuccess || fr < need + tot / 8) {
+        ok = false;
+        break;
+      }
+    }
+    if (ok) return w;
+  }
+  for (auto& d : ctx->devs)
+    if (!d->budget->fits(nt::wcomb_bytes_per_key(nt::kKeyCombNarrow) * nk)) return 0;
+  return nt::kKeyCombNarrow;
+}
+
+
 }  // namespace ntrt
 
 using namespace ntrt;
@@ -156,6 +190,7 @@ static NtSmallModel with_env(NtSmallModel m) {
   m.gpu_call_us = env_or("NT_SMALL_GPU_CALL_US", m.gpu_call_us);
   m.pcie_gbs = env_or("NT_SMALL_PCIE_GBS", m.pcie_gbs);
   m.spawn_us = env_or("NT_SMALL_SPAWN_US", m.spawn_us);
+  m.gpu_keyset_us = env_or("NT_SMALL_GPU_KEYSET_US", m.gpu_keyset_us);
   return m;
 }
 static int calibrate_small(nt_ctx* ctx);
@@ -214,6 +249,16 @@ static int init_common(nt_ctx** out, const std::vector<int>& ords) {
     ctx->devs.push_back(std::move(d));
   }
   if (ctx->devs.empty()) return NT_ENODEV;
+  // NT_KEY_CACHE=<max_keys>[:<admit_after>]: the key registry (nt_set_key_cache)
+  if (const char* e = std::getenv("NT_KEY_CACHE")) {
+    const long k = std::atol(e);
+    const char* c = std::strchr(e, ':');
+    const long a = c ? std::atol(c + 1) : 1;
+    if (k > 0) {
+      const int rc = nt_set_key_cache(ctx.get(), (uint32_t)std::min<long>(k, NT_KEY_CACHE_MAX), (uint32_t)std::max(1L, a));
+      if (rc != NT_OK) return rc;
+    }
+  }
   *out = ctx.release();
   return NT_OK;
 }
@@ -316,12 +361,13 @@ int nt_set_small_call_path(nt_ctx* ctx, int mode, int threads) {
   return NT_OK;
 }
 
-int nt_small_call_model(const nt_ctx* ctx, double* out9) {
-  if (!ctx || !out9) return NT_EINVAL;
+int nt_small_call_model(const nt_ctx* ctx, double* out10) {
+  if (!ctx || !out10) return NT_EINVAL;
   const NtSmallModel& m = ctx->small_model;
-  const double v[9] = {m.cpu_verify_us, m.gpu_verify_us, m.cpu_sha_mbs, m.gpu_lane_mbs, m.gpu_call_us,
-                       m.pcie_gbs,      m.spawn_us,      (double)ctx->small_threads.load(), (double)m.calibrated};
-  std::memcpy(out9, v, sizeof v);
+  const double v[10] = {m.cpu_verify_us, m.gpu_verify_us, m.cpu_sha_mbs, m.gpu_lane_mbs, m.gpu_call_us,
+                        m.pcie_gbs,      m.spawn_us,      (double)ctx->small_threads.load(), (double)m.calibrated,
+                        m.gpu_keyset_us};
+  std::memcpy(out10, v, sizeof v);
   return NT_OK;
 }
 
@@ -647,31 +693,25 @@ int small_threads(const nt_ctx* ctx, uint64_t items) {
   return (int)std::max<uint64_t>(1, std::min(t, items));
 }
 
-// estimated host time of `nsig` verifications on the context's host threads
-bool small_verify(nt_ctx* ctx, uint64_t nsig) {
+// host lane iff the call's estimated host time on the context's threads is
+// below the GPU floor of the kernel it would run (small_model.hpp)
+bool small_verify(nt_ctx* ctx, uint64_t nsig, int kind = nt::kRouteUncached) {
   const int mode = ctx->small_mode.load();
   if (mode == NT_SMALL_ALWAYS) return true;
   if (mode != NT_SMALL_AUTO || !nt::cpu::ready()) return false;
-  const NtSmallModel& m = small_model(ctx);
-  const int T = small_threads(ctx, nsig);
-  const double cpu = std::ceil((double)nsig / T) * m.cpu_verify_us + (T > 1 ? m.spawn_us : 0.0);
-  return cpu < m.gpu_verify_us;
+  return nt::small_verify_on_host(small_model(ctx), nsig, small_threads(ctx, nsig), kind);
 }
 
 bool small_sha(nt_ctx* ctx, uint64_t n, const uint64_t* len) {
   const int mode = ctx->small_mode.load();
   if (mode == NT_SMALL_ALWAYS) return true;
   if (mode != NT_SMALL_AUTO) return false;
-  const NtSmallModel& m = small_model(ctx);
   uint64_t total = 0, mx = 0;
   for (uint64_t i = 0; i < n; ++i) {
     total += len[i];
     mx = std::max(mx, len[i]);
   }
-  const int T = small_threads(ctx, n);
-  const double cpu = std::max((double)mx, (double)total / T) / m.cpu_sha_mbs + (T > 1 ? m.spawn_us : 0.0);
-  const double gpu = m.gpu_call_us + (double)mx / m.gpu_lane_mbs + (double)total / (m.pcie_gbs * 1e3);
-  return cpu < gpu;
+  return nt::small_sha_on_host(small_model(ctx), n, total, mx, small_threads(ctx, n));
 }
 
 void bits_from_bytes(uint8_t* bitmap, const std::vector<uint8_t>& v) {
@@ -757,21 +797,14 @@ int nt_sha512_trunc32(nt_ctx* ctx, const uint8_t* data, const uint64_t* off, con
   }, sha_latency(n, len));
 }
 
-int nt_ed25519_verify_strict(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* sig64,
-                             const uint8_t* msg, const uint64_t* off, const uint64_t* len,
-                             uint64_t n, uint8_t* out_bitmap) {
-  if (!ctx || (n && (!pk32 || !sig64 || !off || !len || !out_bitmap))) return NT_EINVAL;
-  if (n == 0) return NT_OK;
-  if (small_verify(ctx, n)) {
-    std::vector<uint8_t> ok(n);
-    nt::cpu::parallel_for(n, small_threads(ctx, n), [&](uint64_t i) {
-      ok[i] = nt::cpu::verify(nt::kStrict, pk32 + 32 * i, sig64 + 64 * i, msg + off[i], len[i]);
-    });
-    bits_from_bytes(out_bitmap, ok);
-    ctx->calls_host++;
-    return NT_OK;
-  }
-  ctx->calls_gpu++;
+}  // extern "C"
+
+namespace {
+
+// nt_ed25519_verify_strict's GPU body: the uncached verify kernel over the
+// shard's chunks (copies of chunk c + 1 under the kernels of chunk c)
+int verify_strict_gpu(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* sig64, const uint8_t* msg, const uint64_t* off,
+                      const uint64_t* len, uint64_t n, uint8_t* out_bitmap) {
   return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
     NT_CHK(verify_tables(dv));
     const uint64_t m = hi - lo, words = (m + 63) / 64;
@@ -815,22 +848,141 @@ int nt_ed25519_verify_strict(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* si
   }, latency_sized(ctx, (n + ctx->devs.size() - 1) / ctx->devs.size(), nt::verify_round_sigs(ctx->devs[0]->cus)));
 }
 
+int verify_keyset_gpu(nt_ctx* ctx, const KeyDev& kd, int mode, const uint32_t* key_idx, const uint8_t* sig64,
+                      const uint8_t* msg, const uint64_t* off, const uint64_t* len, uint64_t n, uint8_t* out_bitmap);
+
+// Registry lookups (key_table.hpp) of n consecutive 32-byte keys into kid (nt::kKeyMiss where the index does not hold the key), on up to 16 of
+// the host lane's pool threads above 16k keys; returns the misses
+uint64_t reg_lookup(const nt::KeyTable& tab, const uint8_t* pk, uint64_t n, uint32_t* kid) {
+  const uint64_t T = std::min<uint64_t>(16, 1 + n / 16384);
+  std::vector<uint64_t> miss(T, 0);
+  auto work = [&](uint64_t t) {
+    uint64_t m = 0;
+    for (uint64_t i = n * t / T; i < n * (t + 1) / T; ++i) {
+      kid[i] = tab.find(pk + 32 * i);
+      m += kid[i] == nt::kKeyMiss;
+    }
+    miss[t] = m;
+  };
+  if (T == 1) work(0);
+  else nt::cpu::parallel_for_fn(T, (int)T, work);
+  uint64_t m = 0;
+  for (uint64_t x : miss) m += x;
+  return m;
+}
+
+// up to kRegNoteMax keys of the items that missed (kid null: of every item), for the registry's sightings
+std::vector<const uint8_t*> missed_keys(const uint8_t* pk, uint64_t n, const uint32_t* kid) {
+  std::vector<const uint8_t*> v;
+  for (uint64_t i = 0; i < n && v.size() < 4 * kRegNoteMax; ++i)
+    if (!kid || kid[i] == nt::kKeyMiss) v.push_back(pk + 32 * i);
+  return v;
+}
+
+void bits_set(uint8_t* bm, uint64_t i, bool v) {
+  if (v) bm[i >> 3] |= (uint8_t)(1u << (i & 7));
+  else bm[i >> 3] &= (uint8_t)~(1u << (i & 7));
+}
+
+// verify_strict with the registry's snapshot: every item through the key-cache
+// kernel in strict mode (a missed key carries kKeyMiss: unknown, reject), then
+// the misses through the uncached kernel, their verdicts merged
+int verify_strict_reg(nt_ctx* ctx, const RegSnap& snap, const std::vector<uint32_t>& kid, uint64_t miss,
+                      const uint8_t* pk32, const uint8_t* sig64, const uint8_t* msg, const uint64_t* off,
+                      const uint64_t* len, uint64_t n, uint8_t* out_bitmap) {
+  NT_CHK0(verify_keyset_gpu(ctx, snap.dev(), NT_MODE_STRICT, kid.data(), sig64, msg, off, len, n, out_bitmap));
+  if (!miss) return NT_OK;
+  std::vector<uint64_t> idx;
+  idx.reserve(miss);
+  uint64_t bytes = 0, mn = UINT64_MAX, mx = 0;
+  for (uint64_t i = 0; i < n; ++i)
+    if (kid[i] == nt::kKeyMiss) {
+      idx.push_back(i);
+      bytes += len[i];
+      if (len[i]) {
+        mn = std::min(mn, off[i]);
+        mx = std::max(mx, off[i] + len[i]);
+      }
+    }
+  const uint64_t M = idx.size();
+  std::vector<uint8_t> pk(32 * M), sg(64 * M), bm((M + 7) / 8 + 1);
+  std::vector<uint64_t> o(M), l(M);
+  // the misses' messages: gathered when they are a small part of the span they
+  // lie in (a few scattered misses must not copy the whole buffer), else in place
+  const bool gather = mn < mx && bytes < (mx - mn) / 4;
+  std::vector<uint8_t> gm(gather ? bytes + 1 : 0);
+  uint64_t at = 0;
+  for (uint64_t j = 0; j < M; ++j) {
+    const uint64_t i = idx[j];
+    std::memcpy(pk.data() + 32 * j, pk32 + 32 * i, 32);
+    std::memcpy(sg.data() + 64 * j, sig64 + 64 * i, 64);
+    l[j] = len[i];
+    if (gather) {
+      if (len[i]) std::memcpy(gm.data() + at, msg + off[i], len[i]);
+      o[j] = at;
+      at += len[i];
+    } else {
+      o[j] = off[i];
+    }
+  }
+  NT_CHK0(verify_strict_gpu(ctx, pk.data(), sg.data(), gather ? gm.data() : msg, o.data(), l.data(), M, bm.data()));
+  for (uint64_t j = 0; j < M; ++j) bits_set(out_bitmap, idx[j], (bm[j >> 3] >> (j & 7)) & 1);
+  return NT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nt_ed25519_verify_strict(nt_ctx* ctx, const uint8_t* pk32, const uint8_t* sig64,
+                             const uint8_t* msg, const uint64_t* off, const uint64_t* len,
+                             uint64_t n, uint8_t* out_bitmap) {
+  if (!ctx || (n && (!pk32 || !sig64 || !off || !len || !out_bitmap))) return NT_EINVAL;
+  if (n == 0) return NT_OK;
+  // the key registry (nt_set_key_cache): registered keys through the key cache
+  std::shared_ptr<const RegSnap> snap = ctx->reg ? reg_snapshot(ctx) : nullptr;
+  std::vector<uint32_t> kid;
+  uint64_t miss = n;
+  if (snap) {
+    kid.resize(n);
+    miss = reg_lookup(snap->table, pk32, n, kid.data());
+    reg_count(ctx, n - miss, miss);
+  }
+  if (ctx->reg && miss) reg_note_misses(ctx, missed_keys(pk32, n, snap ? kid.data() : nullptr));
+  const bool cached = snap && miss < n;
+  if (small_verify(ctx, n, cached && !miss ? nt::kRouteKeyCache : nt::kRouteUncached)) {
+    std::vector<uint8_t> ok(n);
+    nt::cpu::parallel_for(n, small_threads(ctx, n), [&](uint64_t i) {
+      ok[i] = nt::cpu::verify(nt::kStrict, pk32 + 32 * i, sig64 + 64 * i, msg + off[i], len[i]);
+    });
+    bits_from_bytes(out_bitmap, ok);
+    ctx->calls_host++;
+    return NT_OK;
+  }
+  ctx->calls_gpu++;
+  if (cached) return verify_strict_reg(ctx, *snap, kid, miss, pk32, sig64, msg, off, len, n, out_bitmap);
+  return verify_strict_gpu(ctx, pk32, sig64, msg, off, len, n, out_bitmap);
+}
+
 // Stage certificate groups [glo, ghi) contiguously into pinned host buffers:
 // per signature its key (kw bytes: 32-byte encoding or 4-byte key index) and
 // signature, message offset 32 * (group - glo) and length 32; per group its
 // compacted first / cnt.  Copies are split over host threads by signature count
 // (a config-3 batch stages ~0.6 GB; one thread would take ~50 ms of it).
+// meta = false: hfirst / hcnt already hold the groups' chunk-local starts and counts.
 static void stage_groups(uint64_t glo, uint64_t ghi, const uint64_t* first, const uint32_t* cnt, size_t kw,
                          const uint8_t* keys, const uint8_t* sig64, uint8_t* hkey, uint8_t* hsig, uint64_t* hfirst,
-                         uint32_t* hcnt, bool copy_data) {
+                         uint32_t* hcnt, bool copy_keys, bool copy_sigs, bool meta = true) {
   uint64_t e = 0;
   for (uint64_t g = glo; g < ghi; ++g) {
-    hfirst[g - glo] = e;
-    hcnt[g - glo] = cnt[g];
+    if (meta) {
+      hfirst[g - glo] = e;
+      hcnt[g - glo] = cnt[g];
+    }
     e += cnt[g];
   }
   const uint64_t m = e;
-  if (!copy_data) return;
+  if (!copy_keys && !copy_sigs) return;
   const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   const unsigned T = m < (1u << 16) ? 1u : hw;
   auto work = [&](unsigned t) {
@@ -840,8 +992,8 @@ static void stage_groups(uint64_t glo, uint64_t ghi, const uint64_t* first, cons
     for (; g < ghi && hfirst[g - glo] < shi; ++g) {
       const uint64_t e0 = hfirst[g - glo], c = cnt[g];
       if (!c) continue;
-      std::memcpy(hkey + kw * e0, keys + kw * first[g], kw * c);
-      std::memcpy(hsig + 64 * e0, sig64 + 64 * first[g], 64 * c);
+      if (copy_keys) std::memcpy(hkey + kw * e0, keys + kw * first[g], kw * c);
+      if (copy_sigs) std::memcpy(hsig + 64 * e0, sig64 + 64 * first[g], 64 * c);
     }
   };
   if (T == 1) {
@@ -860,25 +1012,44 @@ namespace {
 
 int dev_index(nt_ctx*, const Device& dv) { return dv.group; }
 
-// Certificate groups through either key form: ks == nullptr -> kw = 32-byte
-// encodings (verify kernel, cofactorless), else kw = 4-byte committee indices
-// (key-cache kernel).  Per shard, groups are staged chunk by chunk into pinned
-// memory (host threads) and copied on the copy stream; chunk c's verify and
-// group-AND launches wait only for chunk c's copies.
-int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* keys, const uint8_t* sig64,
+// A signature whose key the registry index does not hold (verify_groups):
+// its bit in the shard's verdict words, its group and the group's chunk
+struct GroupMiss {
+  uint64_t bit;   // 64 W[c] + chunk-local signature index
+  uint64_t g;     // caller group index
+  uint32_t c;     // chunk
+  uint32_t t;     // index within the group
+};
+
+// Certificate groups through one of three key forms:
+//   kd == nullptr        32-byte encodings, the uncached verify kernel (cofactorless);
+//   kd, tab == nullptr   4-byte committee indices into kd's tables (the key-cache kernel);
+//   kd and tab           32-byte encodings looked up in the registry index `tab` on
+//                        host threads as each chunk is staged, so the chunk carries 4-byte
+//                        indices (68 B per vote over PCIe instead of 96); the signatures
+//                        whose key misses verify afterwards through the uncached kernel
+//                        and their groups' verdicts are recomputed (`missed`: their keys).
+// Per shard, groups are staged chunk by chunk into pinned memory (host threads)
+// and copied on the copy stream; chunk c's verify and group-AND launches wait
+// only for chunk c's copies.
+int verify_groups(nt_ctx* ctx, const KeyDev* kd, const nt::KeyTable* tab, const uint8_t* keys, const uint8_t* sig64,
                   const uint64_t* first, const uint32_t* cnt, const uint8_t* msg32, uint64_t G,
-                  uint8_t* out_group_bitmap, uint8_t* out_sig_bitmap) {
+                  uint8_t* out_group_bitmap, uint8_t* out_sig_bitmap, std::vector<const uint8_t*>* missed = nullptr,
+                  uint64_t* nmissed = nullptr) {
+  const size_t kw = kd && !tab ? 4 : 32;  // key bytes per signature in the caller's array
+  const size_t kdv = kd ? 4 : 32;         // ... and on the device
   uint64_t nsig_total = 0;
   for (uint64_t g = 0; g < G; ++g) nsig_total = std::max(nsig_total, first[g] + cnt[g]);
   if (nsig_total && (!keys || !sig64)) return NT_EINVAL;
   if (out_sig_bitmap) std::memset(out_sig_bitmap, 0, (nsig_total + 7) / 8);
   std::mutex sig_mu;
-  return run_sharded(ctx, G, 64, [&](Device& dv, uint64_t glo, uint64_t ghi) -> int {
-    NT_CHK(ks ? comb_b_for(dv) : verify_tables(dv));
+  std::atomic<uint64_t> nmiss{0};
+  const int rc = run_sharded(ctx, G, 64, [&](Device& dv, uint64_t glo, uint64_t ghi) -> int {
+    NT_CHK(kd ? comb_b_for(dv) : verify_tables(dv));
     const uint64_t gm = ghi - glo;
     uint64_t m = 0;
     for (uint64_t g = glo; g < ghi; ++g) m += cnt[g];
-    const uint64_t R = pipe_round(ks ? nt::keyset_round_sigs(dv.cus) : nt::verify_round_sigs(dv.cus));
+    const uint64_t R = pipe_round(kd ? nt::keyset_round_sigs(dv.cus) : nt::verify_round_sigs(dv.cus));
     const auto ch = plan_group_chunks(glo, ghi, cnt, chunk_targets(m, R));
     const size_t C = ch.size();
     // per chunk: first compacted signature, signature count, verdict-word base
@@ -894,19 +1065,21 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
     // densely packed keys and signatures are copied straight from the caller's
     // arrays: a DMA from nt_host_alloc memory, or HIP's own staged copy from
     // pageable memory (which returns when it is done: run_chunks' staged order);
-    // scattered groups are gathered into the pinned staging on a helper thread
+    // scattered groups are gathered into the pinned staging on a helper thread.
+    // Registry lookups always write their indices into the pinned staging, on the
+    // helper thread ahead of the launches (run_chunks_staged).
     bool direct = m > 0;
     for (uint64_t g = glo; direct && g + 1 < ghi; ++g) direct = first[g + 1] == first[g] + cnt[g];
-    const bool direct_pinned =
-        direct && is_pinned(keys + kw * first[glo], kw * m) && is_pinned(sig64 + 64 * first[glo], 64 * m);
+    const bool direct_pinned = direct && (tab || is_pinned(keys + kw * first[glo], kw * m)) &&
+                               is_pinned(sig64 + 64 * first[glo], 64 * m);
     if (direct && !direct_pinned && std::getenv("NT_GROUPS_GATHER")) direct = false;  // A/B: round-5 staging
-    NT_CHK(dv.h[B_PK].ensure(direct ? 1 : mm * kw));
+    NT_CHK(dv.h[B_PK].ensure(tab ? mm * 4 : (direct ? 1 : mm * kw)));
     NT_CHK(dv.h[B_SIG].ensure(direct ? 1 : mm * 64));
     NT_CHK(dv.h[B_FIRST].ensure(gm * 8));
     NT_CHK(dv.h[B_CNT].ensure(gm * 4));
     NT_CHK(dv.h[B_OUT].ensure(sw * 8 + 8));
     NT_CHK(dv.h[B_OUT2].ensure(gw * 8));
-    NT_CHK(dv.d[B_PK].ensure(mm * kw));
+    NT_CHK(dv.d[B_PK].ensure(mm * kdv));
     NT_CHK(dv.d[B_SIG].ensure(mm * 64));
     NT_CHK(dv.d[B_OFF].ensure(mm * 8));
     NT_CHK(dv.d[B_LEN].ensure(mm * 8));
@@ -915,13 +1088,13 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
     NT_CHK(dv.d[B_CNT].ensure(gm * 4));
     NT_CHK(dv.d[B_OUT].ensure(sw * 8 + 8));
     NT_CHK(dv.d[B_OUT2].ensure(gw * 8));
-    const void* pd_meta = nullptr;
-    if (ks) {
+    const KsTables::PerDev* pd = nullptr;
+    if (kd) {
       uint64_t mc = 0;
       for (size_t c = 0; c < C; ++c) mc = std::max(mc, E[c + 1] - E[c]);
       NT_CHK(dv.ensure_stash(0, mc));
       if (C > 1) NT_CHK(dv.ensure_stash(1, mc));
-      pd_meta = &ks->t->dev[dev_index(ctx, dv)];
+      pd = &kd->t->dev[dev_index(ctx, dv)];
     }
     uint8_t* hkey = dv.h[B_PK].as<uint8_t>();
     uint8_t* hsig = dv.h[B_SIG].as<uint8_t>();
@@ -933,21 +1106,82 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
     NT_CHK(dv.h[B_DATA].ensure(msg_direct ? 1 : gm * 32));
     uint8_t* hmsg = dv.h[B_DATA].as<uint8_t>();
     hipStream_t cs = dv.cstream;
+    std::vector<std::vector<GroupMiss>> miss_c(C);  // written by the copy callbacks only
     NT_TRY(hipMemsetAsync(dv.d[B_OUT].p, 0, sw * 8 + 8, cs));  // before chunk 0's copy-done event
+    // registry lookups of chunk c's keys into hkey (4-byte indices; kKeyMiss = unknown)
+    auto lookup = [&](size_t c) {
+      const uint64_t g0 = ch[c].first, g1 = ch[c].second, gl = g0 - glo, e0 = E[c], mc = E[c + 1] - E[c];
+      const uint64_t* hf = hfirst + gl;  // chunk-local group starts
+      uint32_t* kid = (uint32_t*)hkey + e0;
+      const uint64_t T = std::min<uint64_t>(16, 1 + mc / 16384);
+      std::vector<std::vector<GroupMiss>> part(T);
+      auto work = [&](uint64_t t) {
+        const uint64_t lo = mc * t / T, hi = mc * (t + 1) / T;
+        uint64_t j = (uint64_t)(std::upper_bound(hf, hf + (g1 - g0), lo) - hf) - 1;
+        for (uint64_t e = lo; e < hi; ++e) {
+          while (e >= hf[j] + cnt[g0 + j]) ++j;
+          const uint64_t g = g0 + j, q = e - hf[j];
+          const uint32_t k = tab->find(keys + 32 * (first[g] + q));
+          kid[e] = k;
+          if (k == nt::kKeyMiss) part[t].push_back(GroupMiss{64 * W[c] + e, g, (uint32_t)c, (uint32_t)q});
+        }
+      };
+      if (T == 1) work(0);
+      else nt::cpu::parallel_for_fn(T, (int)T, work);
+      for (auto& v : part) miss_c[c].insert(miss_c[c].end(), v.begin(), v.end());
+    };
+    // Registry lookups run on a thread of their own, chunk by chunk ahead of the
+    // copies: a pageable signature copy (HIP stages it and returns when it is
+    // done) of chunk c then overlaps the lookups of chunk c + 1.
+    struct Ahead {
+      std::thread th;
+      std::mutex mu;
+      std::condition_variable cv;
+      size_t ready = 0;
+      std::atomic<bool> stop{false};
+      ~Ahead() {
+        stop = true;
+        if (th.joinable()) th.join();
+      }
+    } ahead;
+    if (tab && m) {
+      for (size_t c = 0; c < C; ++c) {  // chunk-local group starts (stage_groups leaves them)
+        uint64_t e = 0;
+        for (uint64_t g = ch[c].first; g < ch[c].second; ++g) {
+          hfirst[g - glo] = e;
+          hcnt[g - glo] = cnt[g];
+          e += cnt[g];
+        }
+      }
+      ahead.th = std::thread([&] {
+        for (size_t c = 0; c < C && !ahead.stop; ++c) {
+          if (E[c + 1] > E[c]) lookup(c);
+          std::lock_guard<std::mutex> lk(ahead.mu);
+          ahead.ready = c + 1;
+          ahead.cv.notify_all();
+        }
+      });
+    }
     // direct from pinned memory: every copy is a DMA, so chunk c+1's copies are
     // queued before the host waits on chunk c; direct from pageable memory: chunk
-    // c's kernels are launched before chunk c+1's (synchronous) copies; gathered:
-    // a helper thread stages (host memcpy of keys and signatures) and issues the
-    // chunks ahead of the launches (run_chunks_staged)
+    // c's kernels are launched before chunk c+1's (synchronous) copies; gathered
+    // or looked up: a helper thread stages (host memcpy of keys and signatures,
+    // waits for the chunk's registry lookups) and issues the chunks ahead of the
+    // launches (run_chunks_staged)
     auto copy = [&](size_t c) -> int {
       const uint64_t g0 = ch[c].first, g1 = ch[c].second, gl = g0 - glo, e0 = E[c], mc = E[c + 1] - E[c];
       // chunk-local: hfirst relative to e0; message offsets 32 * (g - g0) made on the device
-      stage_groups(g0, g1, first, cnt, kw, keys, sig64, hkey + kw * e0, hsig + 64 * e0, hfirst + gl, hcnt + gl,
-                   !direct);
+      if (!tab || !direct)
+        stage_groups(g0, g1, first, cnt, kw, keys, sig64, hkey + kw * e0, hsig + 64 * e0, hfirst + gl, hcnt + gl,
+                     !direct && !tab, !direct, !tab);
+      if (tab && mc) {
+        std::unique_lock<std::mutex> lk(ahead.mu);
+        ahead.cv.wait(lk, [&] { return ahead.ready > c; });
+      }
       if (mc) {
-        const uint8_t* sk = direct ? keys + kw * (first[glo] + e0) : hkey + kw * e0;
+        const uint8_t* sk = tab ? hkey + 4 * e0 : direct ? keys + kw * (first[glo] + e0) : hkey + kw * e0;
         const uint8_t* ss = direct ? sig64 + 64 * (first[glo] + e0) : hsig + 64 * e0;
-        NT_TRY(hipMemcpyAsync(dv.d[B_PK].as<uint8_t>() + kw * e0, sk, mc * kw, hipMemcpyHostToDevice, cs));
+        NT_TRY(hipMemcpyAsync(dv.d[B_PK].as<uint8_t>() + kdv * e0, sk, mc * kdv, hipMemcpyHostToDevice, cs));
         NT_TRY(hipMemcpyAsync(dv.d[B_SIG].as<uint8_t>() + 64 * e0, ss, mc * 64, hipMemcpyHostToDevice, cs));
       }
       const uint8_t* sm = msg32 + 32 * g0;
@@ -963,7 +1197,7 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
     auto launch = [&](size_t c) -> int {
       const uint64_t g0 = ch[c].first, g1 = ch[c].second, gl = g0 - glo, e0 = E[c], mc = E[c + 1] - E[c];
       hipStream_t s = dv.cstr((int)c);
-      const uint8_t* dk = dv.d[B_PK].as<uint8_t>() + kw * e0;
+      const uint8_t* dk = dv.d[B_PK].as<uint8_t>() + kdv * e0;
       const uint8_t* dsig = dv.d[B_SIG].as<uint8_t>() + 64 * e0;
       const uint8_t* dmsg = dv.d[B_DATA].as<uint8_t>() + 32 * gl;
       const uint64_t* doff = dv.d[B_OFF].as<uint64_t>() + e0;
@@ -972,14 +1206,13 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
       if (mc) {
         NT_TRY(nt::launch_group_msgs(dv.d[B_FIRST].as<uint64_t>() + gl, dv.d[B_CNT].as<uint32_t>() + gl, g1 - g0,
                                      (uint64_t*)doff, (uint64_t*)dlen, s));
-        if (ks) {
-          const auto& pd = *(const KsTables::PerDev*)pd_meta;
+        if (kd) {
           void* st = (c & 1) ? dv.stash2.p : dv.d[B_STASH].p;
           void* so = (c & 1) ? dv.sort2.p : dv.d[B_SORT].p;
           NT_CHK(dv.keyset_launch(s, st, [&] {
-            return nt::launch_verify_keyset(NT_MODE_COFACTORLESS, ks->bits, (const uint32_t*)dk, dsig, dmsg,
-                                            32 * (g1 - g0), doff, dlen, mc, pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, dv.bbits, st, so,
-                                            dout, dv.cus, s);
+            return nt::launch_verify_keyset(NT_MODE_COFACTORLESS, kd->bits, (const uint32_t*)dk, dsig, dmsg,
+                                            32 * (g1 - g0), doff, dlen, mc, pd->d_meta, pd->d_enc, pd->d_comb,
+                                            kd->nkeys, dv.d_combB, dv.bbits, st, so, dout, dv.cus, s);
           }));
         } else {
           NT_CHK(dv.verify_chunk((int)c, NT_MODE_COFACTORLESS, dk, dsig, dmsg, 32 * (g1 - g0), doff, dlen, mc, dout));
@@ -989,30 +1222,101 @@ int verify_groups(nt_ctx* ctx, const nt_keyset* ks, size_t kw, const uint8_t* ke
                                   dv.d[B_OUT2].as<uint64_t>() + gl / 64, s));
       return NT_OK;
     };
-    NT_CHK(direct || m == 0 ? run_chunks(dv, C, direct_pinned || m == 0, copy, launch)
-                            : run_chunks_staged(dv, C, copy, launch));
+    NT_CHK(!tab && (direct || m == 0) ? run_chunks(dv, C, direct_pinned || m == 0, copy, launch)
+                                      : run_chunks_staged(dv, C, copy, launch));
     hipStream_t s = dv.stream;
     NT_CHK(finish_chunks(dv));
+    if (ahead.th.joinable()) ahead.th.join();  // every chunk's lookups are done: miss_c is final
+    std::vector<GroupMiss> miss;
+    for (auto& v : miss_c) miss.insert(miss.end(), v.begin(), v.end());
     NT_TRY(hipMemcpyAsync(dv.h[B_OUT2].p, dv.d[B_OUT2].p, gw * 8, hipMemcpyDeviceToHost, s));
-    if (out_sig_bitmap && m)
+    if ((out_sig_bitmap || !miss.empty()) && m)
       NT_TRY(hipMemcpyAsync(dv.h[B_OUT].p, dv.d[B_OUT].p, sw * 8, hipMemcpyDeviceToHost, s));
     NT_TRY(hipStreamSynchronize(s));
-    words_to_bitmap(out_group_bitmap + glo / 8, dv.h[B_OUT2].as<uint64_t>(), gm);
+    uint64_t* sbits = dv.h[B_OUT].as<uint64_t>();
+    uint64_t* gbits = dv.h[B_OUT2].as<uint64_t>();
+    if (!miss.empty()) {
+      // the keys the registry does not hold: the uncached kernel over just those
+      // signatures (each over its group's digest, already on the device), then
+      // their bits set and their groups' verdicts recomputed on the host
+      const uint64_t M = miss.size();
+      nmiss += M;
+      NT_CHK(verify_tables(dv));
+      NT_CHK(dv.h[B_PK].ensure(M * 32));
+      NT_CHK(dv.h[B_SIG].ensure(M * 64));
+      NT_CHK(dv.h[B_OFF].ensure(M * 16));
+      NT_CHK(dv.d[B_PK].ensure(M * 32));
+      NT_CHK(dv.d[B_SIG].ensure(M * 64));
+      NT_CHK(dv.d[B_OFF].ensure(M * 16));
+      NT_CHK(dv.d[B_OUT2].ensure(((M + 63) / 64) * 8));
+      uint8_t* pk = dv.h[B_PK].as<uint8_t>();
+      uint8_t* sg = dv.h[B_SIG].as<uint8_t>();
+      uint64_t* ol = dv.h[B_OFF].as<uint64_t>();
+      for (uint64_t j = 0; j < M; ++j) {
+        const uint64_t o = first[miss[j].g] + miss[j].t;
+        std::memcpy(pk + 32 * j, keys + 32 * o, 32);
+        std::memcpy(sg + 64 * j, sig64 + 64 * o, 64);
+        ol[j] = 32 * (miss[j].g - glo);
+        ol[M + j] = 32;
+      }
+      NT_TRY(hipMemcpyAsync(dv.d[B_PK].p, pk, M * 32, hipMemcpyHostToDevice, s));
+      NT_TRY(hipMemcpyAsync(dv.d[B_SIG].p, sg, M * 64, hipMemcpyHostToDevice, s));
+      NT_TRY(hipMemcpyAsync(dv.d[B_OFF].p, ol, M * 16, hipMemcpyHostToDevice, s));
+      const uint64_t R1 = nt::verify_round_sigs(dv.cus, 1);
+      NT_CHK(dv.verify_chunk(0, NT_MODE_COFACTORLESS, dv.d[B_PK].as<uint8_t>(), dv.d[B_SIG].as<uint8_t>(),
+                             dv.d[B_DATA].as<uint8_t>(), 32 * gm, dv.d[B_OFF].as<uint64_t>(),
+                             dv.d[B_OFF].as<uint64_t>() + M, M, dv.d[B_OUT2].as<uint64_t>(), M <= R1 ? 1 : 0));
+      std::vector<uint64_t> mw((M + 63) / 64);
+      NT_TRY(hipMemcpyAsync(mw.data(), dv.d[B_OUT2].p, mw.size() * 8, hipMemcpyDeviceToHost, s));
+      NT_TRY(hipStreamSynchronize(s));
+      std::vector<std::pair<uint64_t, uint32_t>> groups;  // (group, chunk) of every miss
+      for (uint64_t j = 0; j < M; ++j) {
+        if ((mw[j >> 6] >> (j & 63)) & 1) sbits[miss[j].bit >> 6] |= 1ull << (miss[j].bit & 63);
+        groups.emplace_back(miss[j].g, miss[j].c);
+      }
+      std::sort(groups.begin(), groups.end());
+      groups.erase(std::unique(groups.begin(), groups.end()), groups.end());
+      for (const auto& gc : groups) {
+        const uint64_t g = gc.first, b0 = 64 * W[gc.second] + hfirst[g - glo];
+        bool all = true;
+        for (uint64_t q = 0; q < cnt[g] && all; ++q) all = (sbits[(b0 + q) >> 6] >> ((b0 + q) & 63)) & 1;
+        const uint64_t gl = g - glo;
+        if (all) gbits[gl >> 6] |= 1ull << (gl & 63);
+        else gbits[gl >> 6] &= ~(1ull << (gl & 63));
+      }
+      if (missed) {
+        std::lock_guard<std::mutex> lk(sig_mu);
+        for (uint64_t j = 0; j < M && missed->size() < 4 * kRegNoteMax; ++j)
+          missed->push_back(keys + 32 * (first[miss[j].g] + miss[j].t));
+      }
+    }
+    words_to_bitmap(out_group_bitmap + glo / 8, gbits, gm);
     if (out_sig_bitmap && m) {
-      const uint64_t* bits = dv.h[B_OUT].as<uint64_t>();
       std::lock_guard<std::mutex> lk(sig_mu);
       for (size_t c = 0; c < C; ++c) {
         uint64_t e2 = 64 * W[c];
         for (uint64_t g = ch[c].first; g < ch[c].second; ++g)
           for (uint32_t t = 0; t < cnt[g]; ++t, ++e2)
-            if ((bits[e2 >> 6] >> (e2 & 63)) & 1) {
+            if ((sbits[e2 >> 6] >> (e2 & 63)) & 1) {
               const uint64_t o = first[g] + t;
               out_sig_bitmap[o >> 3] |= (uint8_t)(1u << (o & 7));
             }
       }
     }
     return NT_OK;
-  }, latency_sized(ctx, (nsig_total + ctx->devs.size() - 1) / ctx->devs.size(), ks ? nt::keyset_round_sigs(ctx->devs[0]->cus) : nt::verify_round_sigs(ctx->devs[0]->cus)));
+  }, latency_sized(ctx, (nsig_total + ctx->devs.size() - 1) / ctx->devs.size(),
+                   kd ? nt::keyset_round_sigs(ctx->devs[0]->cus) : nt::verify_round_sigs(ctx->devs[0]->cus)));
+  if (nmissed) *nmissed = nmiss.load();
+  return rc;
+}
+
+// any key of the groups' signatures the registry index does not hold
+bool groups_miss(const nt::KeyTable& tab, const uint8_t* pk32, const uint64_t* first, const uint32_t* cnt,
+                 uint64_t G) {
+  for (uint64_t g = 0; g < G; ++g)
+    for (uint32_t q = 0; q < cnt[g]; ++q)
+      if (tab.find(pk32 + 32 * (first[g] + q)) == nt::kKeyMiss) return true;
+  return false;
 }
 
 }  // namespace
@@ -1025,10 +1329,27 @@ int nt_ed25519_verify_batch_groups(nt_ctx* ctx, const uint8_t* pk32, const uint8
                                    uint8_t* out_sig_bitmap) {
   if (!ctx || (G && (!first || !cnt || !msg32 || !out_group_bitmap))) return NT_EINVAL;
   if (G == 0) return NT_OK;
-  uint64_t m = 0;
-  for (uint64_t g = 0; g < G; ++g) m += cnt[g];
-  if (small_verify(ctx, m)) {
-    if (m && (!pk32 || !sig64)) return NT_EINVAL;
+  uint64_t m = 0, nsig = 0;
+  for (uint64_t g = 0; g < G; ++g) {
+    m += cnt[g];
+    nsig = std::max(nsig, first[g] + cnt[g]);
+  }
+  if (m && (!pk32 || !sig64)) return NT_EINVAL;
+  // the key registry (nt_set_key_cache): route by the kernel the call would run --
+  // the key cache when every key hits, the uncached kernel otherwise
+  std::shared_ptr<const RegSnap> snap = ctx->reg ? reg_snapshot(ctx) : nullptr;
+  bool host = small_verify(ctx, m, snap ? nt::kRouteKeyCache : nt::kRouteUncached);
+  if (!host && snap && small_verify(ctx, m, nt::kRouteUncached)) host = groups_miss(snap->table, pk32, first, cnt, G);
+  if (host) {
+    if (ctx->reg) {  // sightings of the keys the registry does not hold yet
+      std::vector<const uint8_t*> ks;
+      for (uint64_t g = 0; g < G && ks.size() < 4 * kRegNoteMax; ++g)
+        for (uint32_t q = 0; q < cnt[g]; ++q) {
+          const uint8_t* p = pk32 + 32 * (first[g] + q);
+          if (!snap || snap->table.find(p) == nt::kKeyMiss) ks.push_back(p);
+        }
+      reg_note_misses(ctx, ks);
+    }
     return host_groups(ctx, sig64, first, cnt, msg32, G, out_group_bitmap, out_sig_bitmap,
                        [&](uint64_t s, uint8_t A[32]) {
                          std::memcpy(A, pk32 + 32 * s, 32);
@@ -1036,7 +1357,23 @@ int nt_ed25519_verify_batch_groups(nt_ctx* ctx, const uint8_t* pk32, const uint8
                        });
   }
   ctx->calls_gpu++;
-  return verify_groups(ctx, nullptr, 32, pk32, sig64, first, cnt, msg32, G, out_group_bitmap, out_sig_bitmap);
+  if (snap) {
+    std::vector<const uint8_t*> missed;
+    uint64_t nmiss = 0;
+    const KeyDev kd = snap->dev();
+    const int rc = verify_groups(ctx, &kd, &snap->table, pk32, sig64, first, cnt, msg32, G, out_group_bitmap,
+                                 out_sig_bitmap, &missed, &nmiss);
+    reg_count(ctx, m - std::min(m, nmiss), nmiss);
+    if (!missed.empty()) reg_note_misses(ctx, missed);
+    return rc;
+  }
+  if (ctx->reg) {  // an empty registry: the first keys of the call are its first sightings
+    std::vector<const uint8_t*> ks;
+    for (uint64_t g = 0; g < G && ks.size() < 4 * kRegNoteMax; ++g)
+      for (uint32_t q = 0; q < cnt[g] && ks.size() < 4 * kRegNoteMax; ++q) ks.push_back(pk32 + 32 * (first[g] + q));
+    reg_note_misses(ctx, ks);
+  }
+  return verify_groups(ctx, nullptr, nullptr, pk32, sig64, first, cnt, msg32, G, out_group_bitmap, out_sig_bitmap);
 }
 
 int nt_ed25519_sign_batch(nt_ctx* ctx, const uint8_t* seed32, const uint8_t* msg,
@@ -1078,39 +1415,6 @@ int nt_ed25519_keypair_batch(nt_ctx* ctx, const uint8_t* seed32, uint64_t n, uin
 }
 
 // ---- committee key cache --------------------------------------------------
-// Comb width of a new key set: the widest of 21 (reduced scalars) / 20 / 18 /
-// 16-bit digits (12 / 13 / 15 / 16 additions per [k]A; 1.61 GB / 872 / 252 /
-// 67 MB per key) that, on every device entry of the context, fits the
-// context's HBM budget beside the comb of B and the tables the entry already
-// holds, and leaves 1/8 of the device's HBM free.  With no width passing the
-// free-memory test the 16-bit combs are tried anyway (hipMalloc decides); 0 =
-// not even those fit the budget.  NT_KEYSET_COMB_BITS=16|18|20|21 forces one.
-static int keyset_comb_bits(nt_ctx* ctx, uint32_t nkeys) {
-  if (const char* e = std::getenv("NT_KEYSET_COMB_BITS")) {
-    const int b = std::atoi(e);
-    if (b == nt::kKeyCombReduced || b == nt::kKeyCombWide || b == nt::kKeyCombMid || b == nt::kKeyCombNarrow)
-      return b;
-  }
-  const uint64_t nk = std::max<uint32_t>(nkeys, 1);
-  for (const int w : {nt::kKeyCombReduced, nt::kKeyCombWide, nt::kKeyCombMid, nt::kKeyCombNarrow}) {
-    const uint64_t comb = nt::wcomb_bytes_per_key(w) * nk;
-    const uint64_t need = comb + nt::wcomb_fill_tmp_bytes_per_key(w) * nt::wcomb_fill_batch(w);
-    bool ok = true;
-    for (auto& d : ctx->devs) {
-      size_t fr = 0, tot = 0;
-      if (!d->budget->fits(comb) || hipSetDevice(d->ordinal) != hipSuccess ||
-          hipMemGetInfo(&fr, &tot) != hipSuccess || fr < need + tot / 8) {
-        ok = false;
-        break;
-      }
-    }
-    if (ok) return w;
-  }
-  for (auto& d : ctx->devs)
-    if (!d->budget->fits(nt::wcomb_bytes_per_key(nt::kKeyCombNarrow) * nk)) return 0;
-  return nt::kKeyCombNarrow;
-}
-
 // Small-call path: key encoding and check mode of one key-cache entry, as
 // the key-cache kernel's loader decodes key_idx (k_keyset.inc KsLoader): in
 // NT_MODE_MIXED bit 31 selects strict; an index >= nkeys is no key (-1, reject).
@@ -1125,7 +1429,10 @@ static int keyset_key(const nt_keyset* ks, int mode, uint32_t kraw, uint8_t A[32
   return m;
 }
 
-int nt_keyset_create(nt_ctx* ctx, const uint8_t* pk32, uint32_t nkeys, nt_keyset** out) {
+}  // extern "C"
+
+// nt_keyset_create at a given key-comb width (0 = the widest that fits)
+static int keyset_create(nt_ctx* ctx, const uint8_t* pk32, uint32_t nkeys, int bits, nt_keyset** out) {
   if (!ctx || !out || (nkeys && !pk32)) return NT_EINVAL;
   *out = nullptr;
   // verification against the set reads the comb of B: it takes its share of the
@@ -1137,7 +1444,7 @@ int nt_keyset_create(nt_ctx* ctx, const uint8_t* pk32, uint32_t nkeys, nt_keyset
   auto ks = std::make_unique<nt_keyset>();
   ks->ctx = ctx;
   ks->nkeys = nkeys;
-  ks->bits = keyset_comb_bits(ctx, nkeys);
+  ks->bits = bits ? bits : keyset_comb_bits(ctx, nkeys);
   if (ks->bits == 0) return NT_ENOMEM;
   ks->flags.assign(nkeys, 0);
   if (nkeys) ks->enc.assign(pk32, pk32 + 32ull * nkeys);
@@ -1178,6 +1485,12 @@ int nt_keyset_create(nt_ctx* ctx, const uint8_t* pk32, uint32_t nkeys, nt_keyset
   return NT_OK;
 }
 
+extern "C" {
+
+int nt_keyset_create(nt_ctx* ctx, const uint8_t* pk32, uint32_t nkeys, nt_keyset** out) {
+  return keyset_create(ctx, pk32, nkeys, 0, out);
+}
+
 void nt_keyset_free(nt_keyset* ks) { delete ks; }
 
 int nt_keyset_flags(const nt_keyset* ks, uint32_t i, uint32_t* flags) {
@@ -1195,28 +1508,15 @@ int nt_keyset_info(const nt_keyset* ks, uint32_t* comb_bits, uint64_t* bytes_per
   return NT_OK;
 }
 
-int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const uint32_t* key_idx,
-                             const uint8_t* sig64, const uint8_t* msg, const uint64_t* off,
-                             const uint64_t* len, uint64_t n, uint8_t* out_bitmap) {
-  if (!ctx || !ks || ks->ctx != ctx || (mode != NT_MODE_STRICT && mode != NT_MODE_COFACTORLESS && mode != NT_MODE_MIXED))
-    return NT_EINVAL;
-  if (n && (!key_idx || !sig64 || !off || !len || !out_bitmap)) return NT_EINVAL;
-  if (n == 0) return NT_OK;
-  if (small_verify(ctx, n)) {
-    std::vector<uint8_t> ok(n);
-    nt::cpu::parallel_for(n, small_threads(ctx, n), [&](uint64_t i) {
-      uint8_t A[32];
-      const int m = keyset_key(ks, mode, key_idx[i], A);
-      ok[i] = m >= 0 && nt::cpu::verify(m, A, sig64 + 64 * i, msg + off[i], len[i]);
-    });
-    bits_from_bytes(out_bitmap, ok);
-    ctx->calls_host++;
-    return NT_OK;
-  }
-  ctx->calls_gpu++;
+}  // extern "C"
+
+namespace {
+// key-cache verification of n (key index, signature, message) items against kd's tables
+int verify_keyset_gpu(nt_ctx* ctx, const KeyDev& kd, int mode, const uint32_t* key_idx, const uint8_t* sig64,
+                      const uint8_t* msg, const uint64_t* off, const uint64_t* len, uint64_t n, uint8_t* out_bitmap) {
   return run_sharded(ctx, n, 64, [&](Device& dv, uint64_t lo, uint64_t hi) -> int {
     NT_CHK(comb_b_for(dv));
-    const auto& pd = ks->t->dev[dev_index(ctx, dv)];
+    const auto& pd = kd.t->dev[dev_index(ctx, dv)];
     const uint64_t m = hi - lo, words = (m + 63) / 64;
     const auto ch = plan_chunks(m, pipe_round(nt::keyset_round_sigs(dv.cus)));
     MsgStage ms;
@@ -1244,10 +1544,10 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
       void* so = (c & 1) ? dv.sort2.p : dv.d[B_SORT].p;
       hipStream_t s = dv.cstr((int)c);
       return dv.keyset_launch(s, st, [&] {
-        return nt::launch_verify_keyset(mode, ks->bits, dv.d[B_PK].as<uint32_t>() + a,
+        return nt::launch_verify_keyset(mode, kd.bits, dv.d[B_PK].as<uint32_t>() + a,
                                         dv.d[B_SIG].as<uint8_t>() + 64 * a, dv.d[B_DATA].as<uint8_t>(), ms.span,
                                         chunk_off(dv, a), chunk_len(dv, a, b), b - a,
-                                        pd.d_meta, pd.d_enc, pd.d_comb, ks->nkeys, dv.d_combB, dv.bbits, st, so,
+                                        pd.d_meta, pd.d_enc, pd.d_comb, kd.nkeys, dv.d_combB, dv.bbits, st, so,
                                         dv.d[B_OUT].as<uint64_t>() + a / 64, dv.cus, s);
       });
     }));
@@ -1257,6 +1557,32 @@ int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const u
     words_to_bitmap(out_bitmap + lo / 8, dv.h[B_OUT].as<uint64_t>(), m);
     return NT_OK;
   }, latency_sized(ctx, (n + ctx->devs.size() - 1) / ctx->devs.size(), nt::keyset_round_sigs(ctx->devs[0]->cus)));
+}
+}  // namespace
+
+extern "C" {
+
+int nt_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int mode, const uint32_t* key_idx,
+                             const uint8_t* sig64, const uint8_t* msg, const uint64_t* off,
+                             const uint64_t* len, uint64_t n, uint8_t* out_bitmap) {
+  if (!ctx || !ks || ks->ctx != ctx || (mode != NT_MODE_STRICT && mode != NT_MODE_COFACTORLESS && mode != NT_MODE_MIXED))
+    return NT_EINVAL;
+  if (n && (!key_idx || !sig64 || !off || !len || !out_bitmap)) return NT_EINVAL;
+  if (n == 0) return NT_OK;
+  if (small_verify(ctx, n, nt::kRouteKeyCache)) {
+    std::vector<uint8_t> ok(n);
+    nt::cpu::parallel_for(n, small_threads(ctx, n), [&](uint64_t i) {
+      uint8_t A[32];
+      const int m = keyset_key(ks, mode, key_idx[i], A);
+      ok[i] = m >= 0 && nt::cpu::verify(m, A, sig64 + 64 * i, msg + off[i], len[i]);
+    });
+    bits_from_bytes(out_bitmap, ok);
+    ctx->calls_host++;
+    return NT_OK;
+  }
+  ctx->calls_gpu++;
+  return verify_keyset_gpu(ctx, KeyDev{ks->t.get(), ks->bits, ks->nkeys}, mode, key_idx, sig64, msg, off, len, n,
+                           out_bitmap);
 }
 
 int nt_ed25519_verify_batch_groups_keyset(nt_ctx* ctx, const nt_keyset* ks, const uint32_t* key_idx,
@@ -1268,13 +1594,14 @@ int nt_ed25519_verify_batch_groups_keyset(nt_ctx* ctx, const nt_keyset* ks, cons
   if (G == 0) return NT_OK;
   uint64_t m = 0;
   for (uint64_t g = 0; g < G; ++g) m += cnt[g];
-  if (small_verify(ctx, m)) {
+  if (small_verify(ctx, m, nt::kRouteKeyCache)) {
     if (m && (!key_idx || !sig64)) return NT_EINVAL;
     return host_groups(ctx, sig64, first, cnt, msg32, G, out_group_bitmap, out_sig_bitmap,
                        [&](uint64_t s, uint8_t A[32]) { return keyset_key(ks, NT_MODE_COFACTORLESS, key_idx[s], A); });
   }
   ctx->calls_gpu++;
-  return verify_groups(ctx, ks, 4, (const uint8_t*)key_idx, sig64, first, cnt, msg32, G, out_group_bitmap,
+  const KeyDev kd{ks->t.get(), ks->bits, ks->nkeys};
+  return verify_groups(ctx, &kd, nullptr, (const uint8_t*)key_idx, sig64, first, cnt, msg32, G, out_group_bitmap,
                        out_sig_bitmap);
 }
 
@@ -1351,6 +1678,19 @@ int nt_dev_ed25519_verify_keyset(nt_ctx* ctx, const nt_keyset* ks, int dev, void
                                     pd.d_enc, pd.d_comb, ks->nkeys, dv->d_combB, dv->bbits, stash, so, d_out_words,
                                     dv->cus, s);
   });
+}
+
+int nt_dev_clock_probe(nt_ctx* ctx, int dev, void* stream, uint32_t iters, uint64_t* d_out2, uint64_t* wall_khz) {
+  Device* dv = dev_of(ctx, dev);
+  if (!dv || !d_out2 || iters == 0) return NT_EINVAL;
+  NT_TRY(hipSetDevice(dv->ordinal));
+  if (wall_khz) {
+    int khz = 0;
+    NT_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dv->ordinal));
+    *wall_khz = (uint64_t)khz;
+  }
+  NT_TRY(nt::launch_clock_probe(iters, dv->cus, d_out2, (hipStream_t)stream));
+  return NT_OK;
 }
 
 int nt_dev_ed25519_sign(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_seed32, const uint8_t* d_msg,
@@ -1440,6 +1780,27 @@ static int calibrate_small(nt_ctx* ctx) {
     }
     if (!(bm & 1)) return NT_EHIP;
     m.gpu_verify_us = median_of(t);
+  }
+  {
+    // the key-cache kernel's floor: one signature through a one-key set (16-bit
+    // key combs, 67 MB, freed after; the floor is the launch and one lane's
+    // serial chain -- 27 comb additions and an inversion -- whatever the width)
+    nt_keyset* ks = nullptr;
+    NT_CHK0(keyset_create(ctx, kPk, 1, nt::kKeyCombNarrow, &ks));
+    const uint64_t off = 0, len = 0;
+    const uint32_t k0 = 0;
+    uint8_t bm = 0;
+    std::vector<double> t;
+    int rc = NT_OK;
+    for (int r = 0; r < 6 && rc == NT_OK; ++r) {
+      const auto a = clk::now();
+      rc = nt_ed25519_verify_keyset(ctx, ks, NT_MODE_STRICT, &k0, kSig, kEmpty, &off, &len, 1, &bm);
+      if (r) t.push_back(us(a));
+    }
+    nt_keyset_free(ks);
+    if (rc != NT_OK) return rc;
+    if (!(bm & 1)) return NT_EHIP;
+    m.gpu_keyset_us = median_of(t);
   }
   {
     uint8_t d[32];

@@ -17,9 +17,12 @@
 
 #include "../../include/ntcrypto.h"
 #include "kernels.hpp"
+#include "key_table.hpp"
+#include "small_model.hpp"
 
 struct nt_ctx;
 namespace ntrt {
+struct KeyReg;
 
 
 #define NT_TRY(expr)                       \
@@ -277,8 +280,12 @@ struct Device {
 
   // Wide combs of nkeys encoded points (host words) into d_comb (device);
   // negate: comb of -P (committee keys) instead of P (the base point).
-  int build_wcombs(int bits, const uint32_t* enc_host, uint32_t nkeys, int negate, uint32_t* d_comb, uint32_t* d_meta) {
+  // s: the stream the build runs on (null = the slot's `stream`; the key
+  // registry's admissions pass a low-priority stream of their own)
+  int build_wcombs(int bits, const uint32_t* enc_host, uint32_t nkeys, int negate, uint32_t* d_comb, uint32_t* d_meta,
+                   hipStream_t s = nullptr) {
     if (nkeys == 0) return NT_OK;
+    if (!s) s = stream;
     const uint32_t batch = std::min<uint32_t>(nkeys, nt::wcomb_fill_batch(bits));
     uint32_t *d_enc = nullptr, *d_bases = nullptr, *d_tmp = nullptr;
     int rc = NT_OK;
@@ -286,10 +293,10 @@ struct Device {
         hipMalloc(&d_bases, nt::wcomb_bases_bytes_per_key(bits) * nkeys) != hipSuccess ||
         hipMalloc(&d_tmp, nt::wcomb_fill_tmp_bytes_per_key(bits) * batch) != hipSuccess) {
       rc = NT_ENOMEM;
-    } else if (hipMemcpyAsync(d_enc, enc_host, 32ull * nkeys, hipMemcpyHostToDevice, stream) != hipSuccess ||
-               nt::launch_wcomb_build(bits, d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, stream) !=
+    } else if (hipMemcpyAsync(d_enc, enc_host, 32ull * nkeys, hipMemcpyHostToDevice, s) != hipSuccess ||
+               nt::launch_wcomb_build(bits, d_enc, nkeys, negate, d_comb, d_meta, d_bases, d_tmp, batch, s) !=
                    hipSuccess ||
-               hipStreamSynchronize(stream) != hipSuccess) {
+               hipStreamSynchronize(s) != hipSuccess) {
       rc = NT_EHIP;
     }
     if (d_enc) (void)hipFree(d_enc);
@@ -403,21 +410,6 @@ struct Device {
 
 }  // namespace ntrt
 
-// Cost model of the small-call path (ntcrypto.cpp: small_verify / small_sha):
-// host-lane and GPU-call costs, calibrated by nt_set_small_call_path on the
-// context's own host threads and device (NT_SMALL_* environment variables
-// override single fields for A/B runs).  The defaults are round-2 measurements.
-struct NtSmallModel {
-  double cpu_verify_us = 36.0;   // one host-lane verify_strict on one thread
-  double gpu_verify_us = 1300.0; // a GPU verify call below one round of resident waves
-  double cpu_sha_mbs = 850.0;    // host-lane SHA-512, one thread
-  double gpu_lane_mbs = 30.0;    // one GPU lane's serial SHA-512 chain
-  double gpu_call_us = 60.0;     // a GPU digest call's fixed cost (launch + copies)
-  double pcie_gbs = 20.0;        // host -> device copy of digest inputs
-  double spawn_us = 15.0;        // waking the host lane's worker pool
-  int calibrated = 0;
-};
-
 struct nt_ctx {
   std::vector<std::unique_ptr<ntrt::Device>> devs;
   uint64_t hbm_budget = 0;   // per device entry (Budget::limit); NT_HBM_BUDGET at init
@@ -426,6 +418,9 @@ struct nt_ctx {
   std::atomic<int> small_mode{NT_SMALL_OFF};
   std::atomic<int> small_threads{1};
   std::atomic<uint64_t> calls_host{0}, calls_gpu{0};
+  // the key registry (nt_set_key_cache; registry.cpp): declared after devs so
+  // that it -- its admission thread and device tables -- goes first
+  std::shared_ptr<ntrt::KeyReg> reg;
 };
 
 namespace ntrt {
@@ -456,6 +451,37 @@ struct KsTables {
     }
   }
 };
+
+// The device tables one key-cache launch reads: a key set's, or a published
+// snapshot of the key registry's (keys >= nkeys verify as unknown -> reject).
+struct KeyDev {
+  const KsTables* t = nullptr;
+  int bits = 0;
+  uint32_t nkeys = 0;
+};
+
+// A published state of the key registry (registry.cpp): the host index of
+// keys 0 .. table.nkeys - 1 and the device tables that hold their combs
+// (allocated for `capacity` keys at the first admission; entries below
+// table.nkeys are never written again, so a call that holds this snapshot
+// reads them while later admissions fill the entries above).
+struct RegSnap {
+  nt::KeyTable table;
+  std::shared_ptr<KsTables> t;
+  int bits = 0;
+  KeyDev dev() const { return KeyDev{t.get(), bits, table.nkeys}; }
+};
+// the published snapshot of ctx's registry, or null (registry off / empty)
+std::shared_ptr<const RegSnap> reg_snapshot(nt_ctx* ctx);
+// keys a call could not find: up to kRegNoteMax distinct ones are counted as
+// sightings (and queued for admission once seen `admit_after` times)
+constexpr uint32_t kRegNoteMax = 256;
+void reg_note_misses(nt_ctx* ctx, const std::vector<const uint8_t*>& keys);
+void reg_count(nt_ctx* ctx, uint64_t hits, uint64_t misses);
+// first-use tables and width choice shared with nt_keyset_create (ntcrypto.cpp)
+int keyset_comb_bits(nt_ctx* ctx, uint32_t nkeys);
+int comb_b_for(Device& dv);
+
 }  // namespace ntrt
 
 struct nt_keyset {

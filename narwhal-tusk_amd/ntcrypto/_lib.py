@@ -35,8 +35,11 @@ EXPORTED = [
     "nt_keyset_free", "nt_keyset_flags", "nt_keyset_info", "nt_ed25519_verify_keyset", "nt_ed25519_verify_batch_groups_keyset",
     "nt_dev_ed25519_verify_keyset", "nt_host_alloc", "nt_host_free", "nt_set_small_call_path", "nt_call_counts",
     "nt_committee_create", "nt_committee_free", "nt_certificates_ingest", "nt_small_call_model",
-    "nt_set_hbm_budget", "nt_memory_info", "nt_dev_stream",
+    "nt_set_hbm_budget", "nt_memory_info", "nt_dev_stream", "nt_set_key_cache", "nt_key_cache_add",
+    "nt_key_cache_sync", "nt_key_cache_info", "nt_dev_clock_probe",
 ]
+KEY_CACHE_INFO_KEYS = ("keys", "max_keys", "comb_bits", "bytes_per_device", "hits", "misses", "admitted", "refused",
+                       "pending", "error")
 MEMORY_INFO_KEYS = ("comb_b_bits", "comb_b_bytes", "key_comb_bytes", "workspace_bytes", "stash_bytes",
                     "staging_bytes", "budget", "held")
 
@@ -102,6 +105,12 @@ def load_library(path=None):
         lib.nt_set_hbm_budget.argtypes = [_vp, ctypes.c_uint64]
         lib.nt_memory_info.argtypes = [_vp, ctypes.c_int, _u64p]
         lib.nt_dev_stream.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_vp)]
+    if hasattr(lib, "nt_set_key_cache"):  # absent from round-5 A/B builds (NTCRYPTO_LIB)
+        lib.nt_set_key_cache.argtypes = [_vp, ctypes.c_uint32, ctypes.c_uint32]
+        lib.nt_key_cache_add.argtypes = [_vp, _u8p, ctypes.c_uint32]
+        lib.nt_key_cache_sync.argtypes = [_vp]
+        lib.nt_key_cache_info.argtypes = [_vp, _u64p]
+        lib.nt_dev_clock_probe.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_uint32, _vp, _u64p]
     _lib = lib
     return lib
 
@@ -194,11 +203,12 @@ class Backend:
         return arr
 
     def small_call_model(self):
-        """The small-call cost model AUTO routes by (nt_small_call_model)."""
-        out = (ctypes.c_double * 9)()
+        """The small-call cost model AUTO routes by (nt_small_call_model): the
+        host-lane rates and one GPU floor per verify kernel (uncached, key cache)."""
+        out = (ctypes.c_double * 10)()
         _check(self.lib.nt_small_call_model(self.ctx, out), "nt_small_call_model")
         keys = ("cpu_verify_us", "gpu_verify_us", "cpu_sha_mbs", "gpu_lane_mbs", "gpu_call_us", "pcie_gbs",
-                "spawn_us", "threads", "calibrated")
+                "spawn_us", "threads", "calibrated", "gpu_keyset_us")
         d = dict(zip(keys, list(out)))
         d["threads"] = int(d["threads"])
         d["calibrated"] = bool(d["calibrated"])
@@ -221,6 +231,36 @@ class Backend:
         p = _vp()
         _check(self.lib.nt_dev_stream(self.ctx, int(dev), int(which), ctypes.byref(p)), "nt_dev_stream")
         return int(p.value)
+
+    # ---- the key registry (nt_set_key_cache): the key cache behind the plain entry points ----
+    def set_key_cache(self, max_keys, admit_after=1):
+        """Enable (max_keys > 0) or disable (0) the context's key registry."""
+        _check(self.lib.nt_set_key_cache(self.ctx, int(max_keys), int(admit_after)), "nt_set_key_cache")
+
+    def key_cache_add(self, pks):
+        """Admit these 32-byte keys now (waits for their tables)."""
+        pks = np.ascontiguousarray(pks, np.uint8).reshape(-1, 32)
+        buf = pks if len(pks) else np.zeros((1, 32), np.uint8)
+        _check(self.lib.nt_key_cache_add(self.ctx, _p(buf), len(pks)), "nt_key_cache_add")
+
+    def key_cache_sync(self):
+        """Wait until queued admissions are published (nt_key_cache_sync)."""
+        _check(self.lib.nt_key_cache_sync(self.ctx), "nt_key_cache_sync")
+
+    def key_cache_info(self):
+        out = np.zeros(10, np.uint64)
+        _check(self.lib.nt_key_cache_info(self.ctx, _p(out, _u64p)), "nt_key_cache_info")
+        d = dict(zip(KEY_CACHE_INFO_KEYS, (int(x) for x in out)))
+        d["error"] = -d["error"]
+        return d
+
+    def dev_clock_probe(self, dev, stream, iters, d_out2):
+        """Enqueue the clock probe (nt_dev_clock_probe) on `stream`; returns the
+        wall clock's rate in kHz.  d_out2: device uint64[2] (cycles, wall ticks)."""
+        khz = np.zeros(1, np.uint64)
+        _check(self.lib.nt_dev_clock_probe(self.ctx, int(dev), stream, int(iters), d_out2, _p(khz, _u64p)),
+               "nt_dev_clock_probe")
+        return int(khz[0])
 
     def call_counts(self):
         """(host-lane calls, GPU calls) of the host entry points so far."""

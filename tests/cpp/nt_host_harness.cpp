@@ -15,6 +15,8 @@
 #include "../../narwhal-tusk_amd/csrc/fe_inv_vt.hpp"
 #include "../../narwhal-tusk_amd/csrc/ks_plan.hpp"
 #include "../../narwhal-tusk_amd/csrc/pipe_plan.hpp"
+#include "../../narwhal-tusk_amd/csrc/key_table.hpp"
+#include "../../narwhal-tusk_amd/csrc/small_model.hpp"
 
 namespace nt {
 unsigned long long g_fe_mul = 0, g_fe_sq = 0;
@@ -541,5 +543,28 @@ unsigned long long nth_fe_invert_cmp(unsigned long long n, unsigned long long se
     bad += std::memcmp(o1, o2, 32) != 0;
   }
   return bad;
+}
+}
+
+// ---- small-call routing (small_model.hpp) and the key registry's host index (key_table.hpp)
+extern "C" {
+// 1 = the host lane serves a verify call of nsig signatures on `threads` threads, given the
+// model fields m[0..3] = cpu_verify_us, spawn_us, gpu_verify_us, gpu_keyset_us; kind 0 =
+// uncached kernel, 1 = key cache
+int nth_small_verify_on_host(const double* m, unsigned long long nsig, int threads, int kind) {
+  NtSmallModel mm;
+  mm.cpu_verify_us = m[0];
+  mm.spawn_us = m[1];
+  mm.gpu_verify_us = m[2];
+  mm.gpu_keyset_us = m[3];
+  return nt::small_verify_on_host(mm, nsig, threads, kind) ? 1 : 0;
+}
+
+// KeyTable over keys[0 .. nkeys) (seed varies the hash), then find() of each of the nq queries
+void nth_key_table_find(const uint8_t* keys, uint32_t nkeys, unsigned long long seed, const uint8_t* q,
+                        unsigned long long nq, uint32_t* out) {
+  nt::KeyTable t;
+  t.build(keys, nkeys, seed);
+  for (unsigned long long i = 0; i < nq; ++i) out[i] = t.find(q + 32 * i);
 }
 }

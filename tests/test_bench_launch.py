@@ -53,7 +53,9 @@ def test_two_rank_bench_on_one_gpu():
                         "--sigs", "8192", "--certs", "2000", "--committee", "10", "--sha-msgs", "256",
                         "--sha-len", "20000", "--no-cpu", "--no-latency", "--no-ingest"],
                        env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
+    # every rank's own error lines first (the launcher's tail shows only the first rank to fail)
+    errs = [x for x in r.stderr.splitlines() if "Error" in x or "error" in x][:40]
+    assert r.returncode == 0, "\n".join(errs) + "\n" + r.stderr[-3000:]
     lines = [json.loads(x) for x in re.findall(r"^\{.*\}$", r.stdout, re.M)]
     assert len(lines) == 1
     d = lines[0]

@@ -1,0 +1,4 @@
+#!/bin/bash
+set -o pipefail
+export TMPDIR=/tmp NT_BENCH_HOST_CERTS=0
+bash tools/ab_env.sh gpurun_out/r05q 3 "--no-ingest --no-latency --no-cpu --no-sha --sigs 65536 --steps 20 --warmup 5" "NT_X=base" "NT_KEYSET_SORT=0" "NT_BENCH_SIDE=0"

@@ -1,0 +1,4 @@
+#!/bin/bash
+set -o pipefail
+export TMPDIR=/tmp NT_BENCH_HOST_CERTS=0 NT_BENCH_SHARDS=0
+bash tools/ab_env.sh gpurun_out/r05w 3 "--no-ingest --no-latency --no-cpu --no-sha --steps 20 --warmup 5" "NT_X=base" "NTCRYPTO_LIB=alt/bhalf/libntcrypto.so" "NTCRYPTO_LIB=alt/khalf/libntcrypto.so"
