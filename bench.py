@@ -1010,8 +1010,11 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                               b["hd2"].data_ptr(), max_len=hlen)
                 hev = torch.cuda.Event()
                 hev.record(side[k])
-            ks.dev_verify(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(), nbytes(b["msgbuf"]),
-                          m_off.data_ptr(), m_len.data_ptr(), V + G, b["mbits"].data_ptr())
+            # the votes' AND per certificate happens in the key-cache kernel's epilogue
+            # (nt_dev_ed25519_verify_keyset_groups): no pack / group-AND launch follows
+            ks.dev_verify_groups(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(),
+                                 nbytes(b["msgbuf"]), m_off.data_ptr(), m_len.data_ptr(), V + G, first.data_ptr(),
+                                 cnt.data_ptr(), G, b["mbits"].data_ptr(), b["gbits"].data_ptr())
             if timed:
                 kev[-1][1].record(st)
             if side and slots(cached) > 1:
@@ -1020,7 +1023,6 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
             else:
                 be.dev_sha512(0, sq, hdr_flat.data_ptr(), nbytes(hdr_flat), h_off.data_ptr(), h_len.data_ptr(), G, b["hd2"].data_ptr(),
                               max_len=hlen)
-            be.dev_group_and(0, sq, first.data_ptr(), cnt.data_ptr(), G, b["mbits"].data_ptr(), b["gbits"].data_ptr())
         else:
             be.dev_verify(0, sq, ntcrypto.NT_MODE_STRICT, tmp_pk.data_ptr(), hsig.data_ptr(), ids.data_ptr(), nbytes(ids),
                           i_off.data_ptr(), i_len.data_ptr(), G, b["hbits"].data_ptr())
@@ -1192,8 +1194,10 @@ def bench_certs(args, torch, dev, be, sp, stream, world, rank, barrier, max_over
                                   % ({21: 12, 20: 13, 18: 15, 16: 16}.get(ks_bits, 0), ks_bits,
                                      ", k taken as k or k - L" if ks_bits == 21 else ""),
                           "launches": "per step: SHA-512 of the certificate digests, 1 NT_MODE_MIXED key-cache verify "
-                                      "(67 votes cofactorless + the header signature strict), SHA-512 of the header "
-                                      "ids (only the verdict needs them), 1 group AND"},
+                                      "(67 votes cofactorless + the header signature strict) whose kernel also ANDs "
+                                      "the votes per certificate (nt_dev_ed25519_verify_keyset_groups: init, key "
+                                      "sort, kernel), SHA-512 of the header ids on a side stream (only the verdict "
+                                      "needs them)"},
             **out}
 
 
@@ -1276,6 +1280,10 @@ def bench_cert_registry(be, pks, vpk, vsig, cdig, G, quorum, expect, barrier, ma
             "sig_verifies_per_s": round(G_total * quorum / (res["pinned"]["ms_per_call"] * 1e-3), 1),
             "key_registry": {"keys": info["keys"], "comb_bits": info["comb_bits"],
                              "gb_per_device": round(info["bytes_per_device"] / 1e9, 2), "build_s": round(build_s, 3),
+                             "alloc_s": round(info["alloc_us"] / 1e6, 3), "comb_build_s": round(info["build_us"] / 1e6, 3),
+                             "alloc_note": "hipMalloc of the registry's tables right after the key set's 161 GB were "
+                                           "freed waits for the driver to clear that memory; the combs themselves "
+                                           "build in comb_build_s",
                              "lookups_hit": after["hits"], "lookups_missed": after["misses"]},
             "note": "nt_ed25519_verify_batch_groups (the plain entry point the crate's verify_batch binds) on %d "
                     "certificates x %d votes per rank, raw 32-byte keys looked up in the context's key registry on "
@@ -1338,8 +1346,9 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream,
                               t["h_len"].data_ptr(), Gs, b["hd2"].data_ptr(), max_len=t["hlen"])
                 hev = torch.cuda.Event()
                 hev.record(side[i % nst])
-            ks.dev_verify(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(), nbytes(b["msgbuf"]),
-                          m_off.data_ptr(), m_len.data_ptr(), Vs + Gs, b["mbits"].data_ptr())
+            ks.dev_verify_groups(0, sq, ntcrypto.NT_MODE_MIXED, mkey.data_ptr(), msig.data_ptr(), b["msgbuf"].data_ptr(),
+                                 nbytes(b["msgbuf"]), m_off.data_ptr(), m_len.data_ptr(), Vs + Gs, t["first"].data_ptr(),
+                                 t["cnt"].data_ptr(), Gs, b["mbits"].data_ptr(), b["gbits"].data_ptr())
             if timed:
                 kev[-1][1].record(st)
             if side:
@@ -1348,8 +1357,6 @@ def bench_cert_shards(args, torch, dev, ks, be, ntcrypto, streams, side, stream,
             else:
                 be.dev_sha512(0, sq, t["hdr_flat"].data_ptr(), nbytes(t["hdr_flat"]), t["h_off"].data_ptr(), t["h_len"].data_ptr(), Gs,
                               b["hd2"].data_ptr(), max_len=t["hlen"])
-            be.dev_group_and(0, sq, t["first"].data_ptr(), t["cnt"].data_ptr(), Gs, b["mbits"].data_ptr(),
-                             b["gbits"].data_ptr())
 
         for i in range(max(1, args.warmup)):
             step(i)

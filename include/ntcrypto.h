@@ -196,15 +196,17 @@ int nt_ed25519_verify_batch_groups_keyset(nt_ctx *ctx, const nt_keyset *ks, cons
  * nt_key_cache_add: admit these keys now (waits for their tables).
  * nt_key_cache_sync: wait until every queued admission is published; returns
  * the registry's error (NT_ENOMEM: its tables did not fit, it admits no more).
- * nt_key_cache_info out10: keys, max_keys, comb bits, device bytes per device
+ * nt_key_cache_info out12: keys, max_keys, comb bits, device bytes per device
  * entry (0 before the first admission), lookups that hit, lookups that missed,
  * keys admitted, keys refused (do not decode / tables failed), admissions
- * pending, -error. */
+ * pending, -error, microseconds the admission thread spent allocating tables
+ * and building combs (the allocation waits for the driver to clear memory
+ * another table just freed: DESIGN.md §6.5). */
 #define NT_KEY_CACHE_MAX 4095u
 int nt_set_key_cache(nt_ctx *ctx, uint32_t max_keys, uint32_t admit_after);
 int nt_key_cache_add(nt_ctx *ctx, const uint8_t *pk32, uint32_t n);
 int nt_key_cache_sync(nt_ctx *ctx);
-int nt_key_cache_info(const nt_ctx *ctx, uint64_t *out10);
+int nt_key_cache_info(const nt_ctx *ctx, uint64_t *out12);
 
 /* ---- certificate ingestion from wire bytes --------------
  * The primary's receiver deserializes every PrimaryMessage with bincode
@@ -357,6 +359,22 @@ int nt_dev_ed25519_verify_keyset(nt_ctx *ctx, const nt_keyset *ks, int dev, void
  * ratio x the wall clock's rate (*wall_khz) is the effective clock.  bench.py
  * brackets its timed regions with it. */
 int nt_dev_clock_probe(nt_ctx *ctx, int dev, void *stream, uint32_t iters, uint64_t *d_out2, uint64_t *wall_khz);
+
+/* The key-cache verification of n signatures that also ANDs their verdicts per
+ * certificate: group g = signatures [d_first[g], d_first[g] + d_cnt[g]) of the
+ * call (d_first non-decreasing; a signature may belong to no group, e.g. a
+ * header signature of a NT_MODE_MIXED call), bit g of d_group_words (ceil(G/64)
+ * words) = every one accepted; an empty group accepts.  The groups' AND and the
+ * verdict words are written by the key-cache kernel itself (one launch chain:
+ * init, key sort, kernel -- no verdict-pack or group-AND launch after it), so a
+ * pipelined caller's next step waits for nothing but this call.  The device
+ * form of nt_ed25519_verify_batch_groups_keyset (Certificate::verify,
+ * primary/src/messages.rs:189-215). */
+int nt_dev_ed25519_verify_keyset_groups(nt_ctx *ctx, const nt_keyset *ks, int dev, void *stream, int mode,
+                                        const uint32_t *d_key_idx, const uint8_t *d_sig64, const uint8_t *d_msg,
+                                        uint64_t msg_bytes, const uint64_t *d_off, const uint64_t *d_len, uint64_t n,
+                                        const uint64_t *d_first, const uint32_t *d_cnt, uint64_t G,
+                                        uint64_t *d_out_words, uint64_t *d_group_words);
 
 /* d_sig64 may be NULL (keygen only; d_msg, d_off, d_len ignored). */
 int nt_dev_ed25519_sign(nt_ctx *ctx, int dev, void *stream, const uint8_t *d_seed32, const uint8_t *d_msg,

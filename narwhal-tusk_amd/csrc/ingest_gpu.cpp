@@ -296,9 +296,9 @@ int ingest_back(Device& dv, IngestState& S, Side& sd, int parity, Chunk& ch, con
   NT_CHK0(dv.keyset_launch(s, st, [&] {
     return nt::launch_verify_keyset(NT_MODE_MIXED, cm.kt->bits, b.keys, (const uint8_t*)b.sigs, b.mbase, mbytes, b.smoff,
                                     b.smlen, nsig, kd.d_meta, kd.d_enc, kd.d_comb, cm.kt->nkeys, dv.d_combB, dv.bbits,
-                                    st, so, sd.words.as<uint64_t>(), dv.cus, s);
+                                    st, so, sd.words.as<uint64_t>(), dv.cus, s, b.gfirst, b.gcnt, m,
+                                    (uint64_t*)b.grp_words);  // the vote groups' AND in the kernel's epilogue
   }));
-  NT_TRY(nt::launch_group_and(b.gfirst, b.gcnt, m, b.sig_words, (uint64_t*)b.grp_words, s));
   NT_TRY(nt::launch_cert_verdict(pd.c, b, gc_round, s));
   NT_TRY(hipMemcpyAsync(S.hcode.as<uint8_t>() + ch.a, b.code, m, hipMemcpyDeviceToHost, s));
   return NT_OK;

@@ -6,8 +6,8 @@
 #define NT_KS_INST(WB)                                                                                          \
   template hipError_t launch_keyset_m<kMixed, 21, WB>(                                                          \
       const KsPlan&, const uint32_t*, const uint8_t*, const uint8_t*, uint64_t, const uint64_t*, const uint64_t*,  \
-      uint64_t, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t, const uint32_t*, void*, uint64_t*,  \
-      const uint32_t*, uint8_t*, uint32_t*, hipStream_t);
+      uint64_t, const uint32_t*, const uint32_t*, const uint32_t*, uint32_t, const uint32_t*, void*,            \
+      const uint32_t*, const KsVerdict&, uint32_t*, hipStream_t);
 namespace nt {
 NT_KS_INST(kBCombBits)
 NT_KS_INST(kBCombFallback)

@@ -677,13 +677,51 @@ KsPlan keyset_plan(uint64_t n, uint32_t cus) {
                                  : ks_plan(n, cus, keyset_per_lane(), force == 1 ? 2 : force);
 }
 
+// A key-cache launch's first kernel: the row counter and, for a key-grouped
+// launch, the bucket lines (count + reservation) zeroed; the verdict words of a
+// key-grouped launch zeroed (its kernel ORs the accepted bits in); each group
+// word set to ones for its groups (the kernel clears a group's bit when one of
+// its signatures rejects; a group reaching past the call's n signatures starts
+// rejected, as k_group_and would find its missing bits clear).  One launch, as
+// the memset it replaces.
+__global__ __launch_bounds__(kBlock) void k_ks_init(uint32_t* __restrict__ ctr, uint32_t nctr,
+                                                   unsigned long long* __restrict__ sw, uint64_t nsw,
+                                                   const uint64_t* __restrict__ gfirst,
+                                                   const uint32_t* __restrict__ gcnt, uint64_t G, uint64_t n,
+                                                   unsigned long long* __restrict__ gw) {
+  aux_priority();
+  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x, stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = t; i < nctr; i += stride) ctr[i] = 0u;
+  for (uint64_t i = t; i < nsw; i += stride) sw[i] = 0ull;
+  const uint64_t ngw = (G + 63) / 64;
+  for (uint64_t w = t; w < ngw; w += stride) {
+    unsigned long long v = G - 64 * w >= 64 ? ~0ull : (1ull << (G - 64 * w)) - 1ull;
+    for (uint64_t g = 64 * w; g < G && g < 64 * w + 64; ++g)
+      if (gfirst[g] + gcnt[g] > n) v &= ~(1ull << (g & 63));
+    gw[w] = v;
+  }
+}
+
+// NT_KEYSET_FUSE=0 (A/B): round 5's epilogue -- verdict bytes + k_pack_bytes for a
+// key-grouped launch and a k_group_and launch for groups
+static bool keyset_fuse() {
+  static const bool on = [] {
+    const char* e = std::getenv("NT_KEYSET_FUSE");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
 hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                                 uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                                 const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
                                 const uint32_t* d_combB, int bbits, void* d_stash, void* d_sort, uint64_t* d_out_words,
-                                uint32_t cus, hipStream_t s) {
+                                uint32_t cus, hipStream_t s, const uint64_t* d_gfirst, const uint32_t* d_gcnt, uint64_t G,
+                                uint64_t* d_group_words) {
   if (!d_sort || !d_stash || !d_combB) return hipErrorInvalidValue;
   if (bbits != kBCombBits && bbits != kBCombFallback) return hipErrorInvalidValue;
+  if (G && (!d_gfirst || !d_gcnt || !d_group_words)) return hipErrorInvalidValue;
+  const bool fuse = keyset_fuse();
   uint32_t* ctr = (uint32_t*)d_sort;
   uint32_t* hist = ctr + kSortHdr / 4;
   uint32_t* p = hist + kSortBuckets * kCtrStride;
@@ -692,13 +730,18 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
     const uint64_t m = n - lo < kKsMaxPerLaunch ? n - lo : kKsMaxPerLaunch;
     const KsPlan pl = keyset_plan(m, cus);
     const uint32_t* perm = nullptr;
-    uint8_t* bytes = nullptr;
     const bool sorted = keyset_sort_enabled() && m >= kSortMin && nkeys + 1 <= kSortBuckets;
-    // the row counter, and for a sorted launch the bucket lines (count + reservation), in one memset
-    hipError_t e = hipMemsetAsync(ctr, 0, sorted ? kSortHdr + 4ull * kCtrStride * (nkeys + 1) : 4, s);
+    const uint64_t gi = fuse && lo == 0 ? G : 0;  // group words: set once, by the first launch's init
+    const uint32_t nctr = sorted ? (uint32_t)((kSortHdr + 4ull * kCtrStride * (nkeys + 1)) / 4) : 1u;
+    const uint64_t nsw = sorted && fuse ? (m + 63) / 64 : 0;
+    const uint64_t most = std::max<uint64_t>(std::max<uint64_t>(nctr, nsw), (gi + 63) / 64);
+    const uint32_t ib = (uint32_t)std::min<uint64_t>(1024, (most + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_ks_init, dim3(ib ? ib : 1), dim3(kBlock), 0, s, ctr, nctr,
+                       (unsigned long long*)(d_out_words + lo / 64), nsw, d_gfirst, d_gcnt, gi, n,
+                       (unsigned long long*)d_group_words);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (sorted) {
-      bytes = (uint8_t*)(p + m);
       const int mixed = mode == kMixed;
       // one tile of kHistTile keys per thread and at most 512 blocks (each flushes its
       // LDS histogram with one global atomic per bucket)
@@ -711,9 +754,12 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
       if ((e = hipGetLastError()) != hipSuccess) return e;
       perm = p;
     }
+    const KsVerdict vd{(unsigned long long*)(d_out_words + lo / 64), sorted && !fuse ? (uint8_t*)(p + m) : nullptr,
+                       fuse ? d_gfirst : nullptr, fuse ? d_gcnt : nullptr, fuse ? G : 0,
+                       (unsigned long long*)d_group_words, lo};
 #define NT_KS_ARGS                                                                                           \
   pl, d_key_idx + lo, d_sig + 64 * lo, d_msg, msg_bytes, d_off + lo, d_len + lo, m, d_meta, d_enc, d_combA, nkeys,     \
-      d_combB, d_stash, d_out_words + lo / 64, perm, bytes, ctr, s
+      d_combB, d_stash, perm, vd, ctr, s
 #define NT_KS_MODES(WA, WB)                                                  \
   (mode == kStrict  ? launch_keyset_m<kStrict, WA, WB>(NT_KS_ARGS)            \
    : mode == kMixed ? launch_keyset_m<kMixed, WA, WB>(NT_KS_ARGS)             \
@@ -729,12 +775,13 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
 #undef NT_KS_MODES
 #undef NT_KS_ARGS
     if (e != hipSuccess) return e;
-    if (perm) {
+    if (vd.bytes) {
       hipLaunchKernelGGL(k_pack_bytes, dim3((uint32_t)((m + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                         (const uint8_t*)bytes, m, (unsigned long long*)(d_out_words + lo / 64));
+                         (const uint8_t*)vd.bytes, m, (unsigned long long*)(d_out_words + lo / 64));
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
   }
+  if (G && !fuse) return launch_group_and(d_gfirst, d_gcnt, G, d_out_words, d_group_words, s);
   return hipSuccess;
 }
 

@@ -35,11 +35,16 @@ hipError_t launch_sign(const uint8_t* d_seed, const uint8_t* d_msg, uint64_t msg
 hipError_t launch_wcomb_build(int bits, const uint32_t* d_enc, uint32_t nkeys, int negate, uint32_t* d_comb,
                               uint32_t* d_meta, uint32_t* d_bases, uint32_t* d_tmp, uint32_t batch,
                               hipStream_t s);
+// Groups (optional, G > 0): the launch also ANDs the verdicts of each group of
+// signatures [d_gfirst[g], d_gfirst[g] + d_gcnt[g]) (d_gfirst non-decreasing)
+// into bit g of d_group_words -- inside the kernel's epilogue (KsVerdict,
+// kernels_common.hpp), no k_group_and launch.
 hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                                 uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                                 const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
                                 const uint32_t* d_combB, int bbits, void* d_stash, void* d_sort, uint64_t* d_out_words,
-                                uint32_t cus, hipStream_t s);
+                                uint32_t cus, hipStream_t s, const uint64_t* d_gfirst = nullptr,
+                                const uint32_t* d_gcnt = nullptr, uint64_t G = 0, uint64_t* d_group_words = nullptr);
 // scratch of launch_verify_keyset: the chunk counter and the key-grouped order (d_sort, required)
 size_t keyset_sort_bytes(uint64_t n);
 // the plan of one key-cache launch over n signatures on a device of `cus` CUs (ks_plan.hpp;

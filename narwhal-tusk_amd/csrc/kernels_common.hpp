@@ -247,6 +247,53 @@ struct KsStash {
   }
 };
 
+// The launch's verdict epilogue (round 6): each signature's
+// verdict goes straight into the caller's 64-bit words -- a ballot store when a
+// row is one word (input order), an atomic OR of its bit when the launch runs
+// in key-grouped order (no verdict bytes, no k_pack_bytes launch) -- and a
+// rejected signature that lies in a certificate group clears that group's bit
+// (the launch's init kernel set every group word to ones), so no k_group_and
+// launch follows.  Groups: G ranges [gfirst[g], gfirst[g] + gcnt[g]) of the
+// launch's signature indices (offset by ibase), gfirst non-decreasing; a
+// signature in no group (a header signature of a mixed launch) only gets its bit.
+struct KsVerdict {
+  unsigned long long* bits;   // the launch's verdict words
+  uint8_t* bytes;             // key-grouped order with the separate pack launch (NT_KEYSET_PACK=1), else null
+  const uint64_t* gfirst;
+  const uint32_t* gcnt;
+  uint64_t G;
+  unsigned long long* gwords;
+  uint64_t ibase;             // index of the launch's signature 0 among the groups' indices
+
+  NT_D NT_INLINE void group_fail(uint64_t i) const {
+    const uint64_t x = ibase + i;
+    if (G == 0 || gfirst[0] > x) return;
+    uint64_t lo = 0, hi = G;  // the last group whose first index is <= x
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (gfirst[mid] <= x) lo = mid;
+      else hi = mid;
+    }
+    if (x < gfirst[lo] + gcnt[lo]) atomicAnd(&gwords[lo >> 6], ~(1ull << (lo & 63)));
+  }
+  // signature i of the launch (key-grouped order: its own index), verdict ok
+  NT_D NT_INLINE void scattered(uint64_t i, uint32_t ok) const {
+    if (bytes) {
+      bytes[i] = (uint8_t)ok;
+    } else if (ok) {
+      atomicOr(&bits[i >> 6], 1ull << (i & 63));
+    }
+    if (!ok) group_fail(i);
+  }
+  // row `row` of the launch in input order (lane = its signature), this lane's verdict ok
+  NT_D NT_INLINE void row(uint64_t row, uint32_t lane, uint32_t ok, uint64_t n) const {
+    const uint64_t gi = 64 * row + lane;
+    const unsigned long long bal = __ballot(ok & (gi < n));
+    if (lane == 0) bits[row] = bal;
+    if (!ok && gi < n) group_fail(gi);
+  }
+};
+
 // Per-mode launchers, explicitly instantiated in k_verify_<mode>.hip and
 // k_keyset_<mode>.hip (one translation unit per kernel family and mode, so
 // the build compiles them in parallel); dispatched by launch_verify /
@@ -261,8 +308,8 @@ template <int MODE, int WA, int WB>
 hipError_t launch_keyset_m(const KsPlan& plan, const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
                            uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n, const uint32_t* d_meta,
                            const uint32_t* d_enc, const uint32_t* d_combA, uint32_t nkeys,
-                           const uint32_t* d_combB, void* d_stash, uint64_t* d_out_words, const uint32_t* d_perm,
-                           uint8_t* d_out_bytes, uint32_t* d_chunk_ctr, hipStream_t s);
+                           const uint32_t* d_combB, void* d_stash, const uint32_t* d_perm, const KsVerdict& vd,
+                           uint32_t* d_chunk_ctr, hipStream_t s);
 int keyset_occupancy();
 
 // Occupancy variants (waves per SIMD the register allocator targets), chosen

@@ -1207,16 +1207,19 @@ int verify_groups(nt_ctx* ctx, const KeyDev* kd, const nt::KeyTable* tab, const 
         NT_TRY(nt::launch_group_msgs(dv.d[B_FIRST].as<uint64_t>() + gl, dv.d[B_CNT].as<uint32_t>() + gl, g1 - g0,
                                      (uint64_t*)doff, (uint64_t*)dlen, s));
         if (kd) {
+          // the key-cache launch ANDs the chunk's groups itself (its kernel's epilogue)
           void* st = (c & 1) ? dv.stash2.p : dv.d[B_STASH].p;
           void* so = (c & 1) ? dv.sort2.p : dv.d[B_SORT].p;
           NT_CHK(dv.keyset_launch(s, st, [&] {
             return nt::launch_verify_keyset(NT_MODE_COFACTORLESS, kd->bits, (const uint32_t*)dk, dsig, dmsg,
                                             32 * (g1 - g0), doff, dlen, mc, pd->d_meta, pd->d_enc, pd->d_comb,
-                                            kd->nkeys, dv.d_combB, dv.bbits, st, so, dout, dv.cus, s);
+                                            kd->nkeys, dv.d_combB, dv.bbits, st, so, dout, dv.cus, s,
+                                            dv.d[B_FIRST].as<uint64_t>() + gl, dv.d[B_CNT].as<uint32_t>() + gl,
+                                            g1 - g0, dv.d[B_OUT2].as<uint64_t>() + gl / 64);
           }));
-        } else {
-          NT_CHK(dv.verify_chunk((int)c, NT_MODE_COFACTORLESS, dk, dsig, dmsg, 32 * (g1 - g0), doff, dlen, mc, dout));
+          return NT_OK;
         }
+        NT_CHK(dv.verify_chunk((int)c, NT_MODE_COFACTORLESS, dk, dsig, dmsg, 32 * (g1 - g0), doff, dlen, mc, dout));
       }
       NT_TRY(nt::launch_group_and(dv.d[B_FIRST].as<uint64_t>() + gl, dv.d[B_CNT].as<uint32_t>() + gl, g1 - g0, dout,
                                   dv.d[B_OUT2].as<uint64_t>() + gl / 64, s));
@@ -1691,6 +1694,35 @@ int nt_dev_clock_probe(nt_ctx* ctx, int dev, void* stream, uint32_t iters, uint6
   }
   NT_TRY(nt::launch_clock_probe(iters, dv->cus, d_out2, (hipStream_t)stream));
   return NT_OK;
+}
+
+int nt_dev_ed25519_verify_keyset_groups(nt_ctx* ctx, const nt_keyset* ks, int dev, void* stream, int mode,
+                                        const uint32_t* d_key_idx, const uint8_t* d_sig64, const uint8_t* d_msg,
+                                        uint64_t msg_bytes, const uint64_t* d_off, const uint64_t* d_len, uint64_t n,
+                                        const uint64_t* d_first, const uint32_t* d_cnt, uint64_t G,
+                                        uint64_t* d_out_words, uint64_t* d_group_words) {
+  Device* dv = dev_of(ctx, dev);
+  if (!dv || !ks || ks->ctx != ctx || (mode != NT_MODE_STRICT && mode != NT_MODE_COFACTORLESS && mode != NT_MODE_MIXED))
+    return NT_EINVAL;
+  if (n && (!d_key_idx || !d_sig64 || !d_msg || !d_off || !d_len || !d_out_words)) return NT_EINVAL;
+  if (G && (!d_first || !d_cnt || !d_group_words)) return NT_EINVAL;
+  NT_TRY(hipSetDevice(dv->ordinal));
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) return G ? (nt::launch_group_and(d_first, d_cnt, G, d_out_words, d_group_words, s) == hipSuccess
+                              ? NT_OK : NT_EHIP)
+                       : NT_OK;
+  const auto& pd = ks->t->dev[dev];
+  std::lock_guard<std::mutex> lk(dv->mu);
+  NT_CHK(comb_b_for(*dv));
+  const int k = (int)(dv->ks_calls++ & 1u);
+  NT_CHK(dv->ensure_stash(k, n));
+  void* stash = k ? dv->stash2.p : dv->d[B_STASH].p;
+  void* so = k ? dv->sort2.p : dv->d[B_SORT].p;
+  return dv->keyset_launch(s, stash, [&] {
+    return nt::launch_verify_keyset(mode, ks->bits, d_key_idx, d_sig64, d_msg, msg_bytes, d_off, d_len, n, pd.d_meta,
+                                    pd.d_enc, pd.d_comb, ks->nkeys, dv->d_combB, dv->bbits, stash, so, d_out_words,
+                                    dv->cus, s, d_first, d_cnt, G, d_group_words);
+  });
 }
 
 int nt_dev_ed25519_sign(nt_ctx* ctx, int dev, void* stream, const uint8_t* d_seed32, const uint8_t* d_msg,

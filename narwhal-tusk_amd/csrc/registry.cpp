@@ -55,6 +55,7 @@ struct KeyReg {
   int error = NT_OK;                    // first failure of an admission (the registry then stops admitting)
   std::vector<hipStream_t> streams;     // one low-priority stream per device entry (admission builds)
   std::atomic<uint64_t> hits{0}, misses{0}, admitted{0}, nrefused{0};
+  uint64_t alloc_us = 0, build_us = 0;  // time the worker spent allocating tables / building combs
   std::thread worker;
 
   ~KeyReg() {
@@ -158,13 +159,15 @@ struct KeyReg {
       if (!ok.empty() && !t) rc = allocate();
       const auto t1 = std::chrono::steady_clock::now();
       if (rc == NT_OK && !ok.empty()) rc = build(ok, nk);
+      const auto t2 = std::chrono::steady_clock::now();
       if (std::getenv("NT_REG_TRACE")) {  // diagnosis: where an admission's time goes
-        const auto t2 = std::chrono::steady_clock::now();
         std::fprintf(stderr, "[registry] %zu keys (%zu refused): allocate %.1f ms, build %.1f ms, rc %d\n", ok.size(),
                      bad.size(), std::chrono::duration<double, std::milli>(t1 - t0).count(),
                      std::chrono::duration<double, std::milli>(t2 - t1).count(), rc);
       }
       lk.lock();
+      alloc_us += (uint64_t)std::chrono::duration<double, std::micro>(t1 - t0).count();
+      build_us += (uint64_t)std::chrono::duration<double, std::micro>(t2 - t1).count();
       building = false;
       for (const Key32& key : batch) pending.erase(key);
       for (const Key32& key : bad) refused.insert(key);
@@ -273,9 +276,9 @@ int nt_key_cache_sync(nt_ctx* ctx) {
   return r->error;
 }
 
-int nt_key_cache_info(const nt_ctx* ctx, uint64_t* out10) {
-  if (!ctx || !out10) return NT_EINVAL;
-  uint64_t v[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+int nt_key_cache_info(const nt_ctx* ctx, uint64_t* out12) {
+  if (!ctx || !out12) return NT_EINVAL;
+  uint64_t v[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   std::shared_ptr<KeyReg> r = ctx->reg;
   if (r) {
     std::lock_guard<std::mutex> lk(r->mu);
@@ -289,8 +292,10 @@ int nt_key_cache_info(const nt_ctx* ctx, uint64_t* out10) {
     v[7] = r->nrefused.load();
     v[8] = r->pending.size();
     v[9] = (uint64_t)(-(int64_t)r->error);
+    v[10] = r->alloc_us;
+    v[11] = r->build_us;
   }
-  std::memcpy(out10, v, sizeof v);
+  std::memcpy(out12, v, sizeof v);
   return NT_OK;
 }
 

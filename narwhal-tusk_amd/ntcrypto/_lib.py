@@ -36,10 +36,10 @@ EXPORTED = [
     "nt_dev_ed25519_verify_keyset", "nt_host_alloc", "nt_host_free", "nt_set_small_call_path", "nt_call_counts",
     "nt_committee_create", "nt_committee_free", "nt_certificates_ingest", "nt_small_call_model",
     "nt_set_hbm_budget", "nt_memory_info", "nt_dev_stream", "nt_set_key_cache", "nt_key_cache_add",
-    "nt_key_cache_sync", "nt_key_cache_info", "nt_dev_clock_probe",
+    "nt_key_cache_sync", "nt_key_cache_info", "nt_dev_clock_probe", "nt_dev_ed25519_verify_keyset_groups",
 ]
 KEY_CACHE_INFO_KEYS = ("keys", "max_keys", "comb_bits", "bytes_per_device", "hits", "misses", "admitted", "refused",
-                       "pending", "error")
+                       "pending", "error", "alloc_us", "build_us")
 MEMORY_INFO_KEYS = ("comb_b_bits", "comb_b_bytes", "key_comb_bytes", "workspace_bytes", "stash_bytes",
                     "staging_bytes", "budget", "held")
 
@@ -111,6 +111,8 @@ def load_library(path=None):
         lib.nt_key_cache_sync.argtypes = [_vp]
         lib.nt_key_cache_info.argtypes = [_vp, _u64p]
         lib.nt_dev_clock_probe.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_uint32, _vp, _u64p]
+        lib.nt_dev_ed25519_verify_keyset_groups.argtypes = [_vp, _vp, ctypes.c_int, _vp, ctypes.c_int, _vp, _vp, _vp,
+                                                            _u64, _vp, _vp, _u64, _vp, _vp, _u64, _vp, _vp]
     _lib = lib
     return lib
 
@@ -248,7 +250,7 @@ class Backend:
         _check(self.lib.nt_key_cache_sync(self.ctx), "nt_key_cache_sync")
 
     def key_cache_info(self):
-        out = np.zeros(10, np.uint64)
+        out = np.zeros(12, np.uint64)
         _check(self.lib.nt_key_cache_info(self.ctx, _p(out, _u64p)), "nt_key_cache_info")
         d = dict(zip(KEY_CACHE_INFO_KEYS, (int(x) for x in out)))
         d["error"] = -d["error"]
@@ -432,6 +434,15 @@ class Keyset:
         if with_sig_bits:
             return _unpack(gb, G), _unpack(sb, nsig)
         return _unpack(gb, G)
+
+    def dev_verify_groups(self, dev, stream, mode, d_key_idx, d_sig, d_msg, msg_bytes, d_off, d_len, n, d_first,
+                          d_cnt, G, d_out, d_group_out):
+        """Key-cache verification + the AND per certificate group in one launch chain
+        (nt_dev_ed25519_verify_keyset_groups): no verdict-pack / group-AND launch after it."""
+        _check(self.be.lib.nt_dev_ed25519_verify_keyset_groups(self.be.ctx, self.h, dev, stream, mode, d_key_idx, d_sig,
+                                                               d_msg, int(msg_bytes), d_off, d_len, n, d_first, d_cnt,
+                                                               int(G), d_out, d_group_out),
+               "nt_dev_ed25519_verify_keyset_groups")
 
     def dev_verify(self, dev, stream, mode, d_key_idx, d_sig, d_msg, msg_bytes, d_off, d_len, n, d_out):
         _check(self.be.lib.nt_dev_ed25519_verify_keyset(self.be.ctx, self.h, dev, stream, mode, d_key_idx, d_sig,

@@ -535,3 +535,72 @@ def test_device_api_out_of_bounds_items(be, corpus):
     assert not b["dg"][bad].any() and np.array_equal(b["dg"][~bad], g["dg"][~bad])
     assert np.array_equal(b["pk"], g["pk"])
     assert not b["sig"][bad].any() and np.array_equal(b["sig"][~bad], g["sig"][~bad])
+
+
+@pytest.mark.parametrize("reps", [1, 1400])
+def test_keyset_device_groups_fused(be, monkeypatch, reps):
+    """nt_dev_ed25519_verify_keyset_groups: the key-cache launch ANDs each
+    certificate group's verdicts in its kernel epilogue (no pack / group-AND
+    launch).  The golden groups fixture (0..67 votes, corrupted s, all-zero
+    vote, torsion-shifted R) tiled once (input-order launch) and 1,400 times
+    (~75k signatures: key-grouped order, atomic verdict bits), plus signatures
+    in no group at the end (header signatures of a mixed launch), empty groups
+    and a group that reaches past the call's signatures (rejects): group and
+    signature words equal nt_dev_ed25519_verify_keyset + nt_dev_group_and and
+    the fixture's verdicts."""
+    import ntcrypto
+    import torch
+    monkeypatch.setenv("NT_KEYSET_COMB_BITS", "16")
+    g = np.load(os.path.join(GOLD, "batch_groups.npz"))
+    uniq, inv = np.unique(g["pk"], axis=0, return_inverse=True)
+    ks = be.keyset(uniq)
+    nsig = len(g["pk"])
+    first = np.concatenate([g["first"] + r * nsig for r in range(reps)]).astype(np.uint64)
+    cnt = np.tile(g["cnt"], reps).astype(np.uint32)
+    G = len(cnt)
+    kidx = np.tile(inv.astype(np.uint32).ravel(), reps)
+    sig = np.tile(g["sig"], (reps, 1))
+    msg32 = np.tile(g["msg32"], (reps, 1))
+    goff = np.concatenate([np.full(int(c), 32 * gi, np.uint64) for gi, c in enumerate(cnt)])
+    assert len(goff) == nsig * reps
+    # 40 extra signatures in no group (copies of the first ones), then two more groups:
+    # an empty one and one reaching past the call's signatures
+    n = nsig * reps + 40
+    kidx = np.concatenate([kidx, kidx[:40]])
+    sig = np.concatenate([sig, sig[:40]])
+    goff = np.concatenate([goff, goff[:40]])
+    first = np.concatenate([first, [n, n - 3]]).astype(np.uint64)
+    cnt = np.concatenate([cnt, [0, 5]]).astype(np.uint32)
+    G2 = G + 2
+    # group first indices must be non-decreasing: the last group starts at n - 3 < n
+    first[-2] = n - 3
+    dev = torch.device("cuda", 0)
+    t = {"k": torch.from_numpy(kidx.view(np.int32)).to(dev), "sig": torch.from_numpy(sig).to(dev),
+         "msg": torch.from_numpy(msg32.reshape(-1)).to(dev), "off": torch.from_numpy(goff.view(np.int64)).to(dev),
+         "len": torch.full((n,), 32, dtype=torch.int64, device=dev),
+         "first": torch.from_numpy(first.view(np.int64)).to(dev), "cnt": torch.from_numpy(cnt.view(np.int32)).to(dev)}
+    w1 = torch.full(((n + 63) // 64 + 1,), -1, dtype=torch.int64, device=dev)   # garbage: the call owns the words
+    gw1 = torch.full(((G2 + 63) // 64 + 1,), 0x5A5A, dtype=torch.int64, device=dev)
+    w2 = torch.zeros_like(w1)
+    gw2 = torch.zeros_like(gw1)
+    st = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    args = (0, st.cuda_stream, ntcrypto.NT_MODE_COFACTORLESS, t["k"].data_ptr(), t["sig"].data_ptr(), t["msg"].data_ptr(),
+            nbytes(t["msg"]), t["off"].data_ptr(), t["len"].data_ptr(), n)
+    ks.dev_verify_groups(*args, t["first"].data_ptr(), t["cnt"].data_ptr(), G2, w1.data_ptr(), gw1.data_ptr())
+    ks.dev_verify(*args, w2.data_ptr())
+    be.dev_group_and(0, st.cuda_stream, t["first"].data_ptr(), t["cnt"].data_ptr(), G2, w2.data_ptr(), gw2.data_ptr())
+    st.synchronize()
+    words = (n + 63) // 64
+    s1 = np.unpackbits(w1.cpu().numpy()[:words].view(np.uint8), bitorder="little")[:n].astype(bool)
+    s2 = np.unpackbits(w2.cpu().numpy()[:words].view(np.uint8), bitorder="little")[:n].astype(bool)
+    assert np.array_equal(s1, s2)
+    gws = (G2 + 63) // 64
+    b1 = np.unpackbits(gw1.cpu().numpy()[:gws].view(np.uint8), bitorder="little")
+    b2 = np.unpackbits(gw2.cpu().numpy()[:gws].view(np.uint8), bitorder="little")
+    assert np.array_equal(b1[:G2], b2[:G2])
+    assert not b1[G2:].any()  # bits past the last group stay clear
+    assert np.array_equal(b1[:G], np.tile(g["expect"], reps).astype(bool))
+    # the last group reaches 2 signatures past n: rejected whatever its signatures' verdicts
+    assert not b1[G2 - 1]
+    ks.close()

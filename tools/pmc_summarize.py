@@ -18,7 +18,7 @@ import os
 import sys
 
 KERNELS = {"k_ed25519_verify_keyset": "verify_keyset", "k_ed25519_verify<": "verify", "k_sha512": "sha512",
-           "k_ed25519_sign": "sign", "k_group_and": "group_and"}
+           "k_ed25519_sign": "sign", "k_group_and": "group_and", "k_clock_probe": "clock_probe"}
 
 
 def kname(k):
