@@ -57,8 +57,8 @@ METRIC = "Ed25519 verifies/sec + SHA-512 GB/s at 1/2/4/8 MI355X vs dalek host-co
 MAD_PEAK_TS = 256 * 4 * 64 * 2.4e9 / 4 / 1e12  # v_mad_u64_u32: 4 cycles per wave64 per SIMD
 MAD_MEASURED_TS = 32.80  # profiles/r01_alu_rate.txt (tools/microbench): 4.80 cycles per wave64 per SIMD
 HBM_PEAK_GBS = 8000.0
-PMC_PROFILE = os.path.join("r05", "pmc_verify_sha.json")  # tools/profile_round.sh + tools/pmc_summarize.py
-PMC_KEYSET_PROFILE = os.path.join("r05", "pmc_keyset.json")  # cfg3 key-cache launch (streamed rows)
+PMC_PROFILE = os.path.join("r06", "pmc_verify_sha.json")  # tools/runs/r06/r06p.sh + tools/pmc_summarize.py
+PMC_KEYSET_PROFILE = os.path.join("r06", "pmc_keyset.json")  # cfg3 key-cache launch (streamed rows)
 PMC_N = 1_000_000  # signatures per launch in that profile (the default config-2 run)
 SODIUM = "/opt/conda/lib/libsodium.so.23"
 
@@ -451,23 +451,32 @@ def main():
                               "profiles/%s (a separate rocprofv3 --pmc run of the same build, on another box); "
                               "run_clock is this run's own" % PMC_PROFILE}
     run_ghz = (clk_before + clk_after) / 2
+    # the kernel's own clock relative to the probe's, both measured in one process (the PMC profile's
+    # GRBM clocks: profiles/r06/clock_probe_calibration_r06p.txt)
+    ratio = probe_ratio(pv, prof)
+    kclk = run_ghz * ratio if ratio else None
     roofline["run_clock"] = {"probe_ghz_before": round(clk_before, 3), "probe_ghz_after": round(clk_after, 3),
                              "probe_ghz": round(run_ghz, 3),
+                             "kernel_over_probe": round(ratio, 4) if ratio else None,
+                             "kernel_clock_est_ghz": round(kclk, 3) if kclk else None,
                              "note": "nt_dev_clock_probe right before and right after the one-stream timed region on "
                                      "its stream (ClockProbe): the shader clock this box holds under a verify-like "
-                                     "v_mad_u64_u32 load in this run"}
-    roofline["frac_at_run_clock"] = round(achieved / (MAD_PEAK_TS * run_ghz / 2.4), 4)
-    roofline["kernel_mcycles_at_run_clock"] = round(kernel_ms * run_ghz * 1e3, 1)
+                                     "v_mad_u64_u32 load in this run; kernel_clock_est = probe x kernel_over_probe "
+                                     "(the two GRBM clocks of %s, one process)" % PMC_PROFILE}
+    roofline["frac_at_run_clock"] = round(achieved / (MAD_PEAK_TS * (kclk or run_ghz) / 2.4), 4)
+    roofline["kernel_mcycles_at_run_clock"] = round(kernel_ms * (kclk or run_ghz) * 1e3, 1)
     # round 5's driver run: 11.308 ms per 1M launch (BENCH_r05.json); its clock was not measured
     # in that run -- the r05b PMC profile's effective clock of the same launch (another box) stands in
     r05 = {"kernel_ms": 11.308, "clock_ghz": 1.979}
+    now_clk = kclk or run_ghz
     roofline["vs_r05"] = {"kernel_ms_r05": r05["kernel_ms"], "kernel_ms": round(kernel_ms, 3),
                           "time_ratio_r05_over_now": round(r05["kernel_ms"] / kernel_ms, 4),
-                          "clock_r05_ghz": r05["clock_ghz"], "clock_now_ghz": round(run_ghz, 3),
-                          "cycle_ratio_r05_over_now": round(r05["kernel_ms"] * r05["clock_ghz"] / (kernel_ms * run_ghz), 4),
-                          "note": "time_ratio > 1: this run's launch is faster; cycle_ratio normalises both by their "
-                                  "clock (r05: the PMC effective clock of its profile, no run clock existed; now: "
-                                  "the run's probe) -- ~1 means the same instruction stream at a different clock"}
+                          "clock_r05_ghz": r05["clock_ghz"], "clock_now_ghz": round(now_clk, 3),
+                          "cycle_ratio_r05_over_now": round(r05["kernel_ms"] * r05["clock_ghz"] / (kernel_ms * now_clk), 4),
+                          "note": "time_ratio > 1: this run's launch is faster; cycle_ratio normalises both by the "
+                                  "kernel's clock (r05: the GRBM clock of its PMC profile, no run clock existed; now: "
+                                  "this run's probe x kernel_over_probe) -- ~1 means the same instruction stream at a "
+                                  "different clock"}
 
     # the other two halves of the metric, filled in when their configs have run, so
     # that they sit near the front of the line (a reader of its first few hundred
@@ -1405,7 +1414,9 @@ def keyset_roofline(launch_ms, step_ms, nsig, clk=None):
     except Exception:
         return None
     achieved = mads * nsig / (kernel_ms * 1e-3) / 1e12
-    pk = (load_profile(PMC_KEYSET_PROFILE) or {}).get("kernels", {}).get("verify_keyset", {})
+    kprof = load_profile(PMC_KEYSET_PROFILE) or {}
+    pk = kprof.get("kernels", {}).get("verify_keyset", {})
+    ratio = probe_ratio(pk, kprof)
     pkl = pk.get("per_launch", {})
     grid = pk.get("grid")
     return {"bound": "valu", "kernel": "k_ed25519_verify_keyset<mixed>", "kernel_ms": round(kernel_ms, 3),
@@ -1426,8 +1437,11 @@ def keyset_roofline(launch_ms, step_ms, nsig, clk=None):
                           "profiles/%s (a separate rocprofv3 --pmc run, another box); run_clock is this run's own"
                           % PMC_KEYSET_PROFILE,
             **({"run_clock": {"probe_ghz_before": round(clk[0], 3), "probe_ghz_after": round(clk[1], 3),
-                              "probe_ghz": round(sum(clk) / 2, 3)},
-                "frac_at_run_clock": round(achieved / (MAD_PEAK_TS * sum(clk) / 2 / 2.4), 4)} if clk else {})}
+                              "probe_ghz": round(sum(clk) / 2, 3),
+                              "kernel_over_probe": round(ratio, 4) if ratio else None,
+                              "kernel_clock_est_ghz": round(sum(clk) / 2 * ratio, 3) if ratio else None},
+                "frac_at_run_clock": round(achieved / (MAD_PEAK_TS * sum(clk) / 2 * (ratio or 1.0) / 2.4), 4)}
+               if clk else {})}
 
 
 def bench_latency(be, pk_h, sig_h, msg_h, L):
@@ -1909,6 +1923,15 @@ def mads_per_verify(msg_len):
             d = json.load(f)
         return int(d["verify_strict_mads"])
     except Exception:
+        return None
+
+
+def probe_ratio(kernel_entry, prof):
+    """A kernel's GRBM clock / the clock probe's GRBM clock in one PMC profile
+    (the same process), or None"""
+    try:
+        return kernel_entry["effective_clock_ghz"] / prof["kernels"]["clock_probe"]["effective_clock_ghz"]
+    except (KeyError, TypeError, ZeroDivisionError):
         return None
 
 
