@@ -48,7 +48,11 @@ struct KeyTable {
     for (uint32_t s = home(h0);; s = (s + 1) & mask) {
       const uint32_t k = idx[s];
       if (k == kKeyMiss) return kKeyMiss;
-      if (head[s] == h0 && std::memcmp(enc.data() + 32ull * k + 8, pk + 8, 24) == 0) return k;
+      if (head[s] == h0) {
+        const uint8_t* e = enc.data() + 32ull * k;  // the other 24 bytes as three words
+        if (((load64(e + 8) ^ load64(pk + 8)) | (load64(e + 16) ^ load64(pk + 16)) | (load64(e + 24) ^ load64(pk + 24))) == 0)
+          return k;
+      }
     }
   }
 

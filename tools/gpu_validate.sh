@@ -2,8 +2,9 @@
 # One GPU session (run through gpurun) for a tree built here.  Steps, chained so
 # the first failure ends the session; every GPU step under its own time limit.
 #   bash tools/gpu_validate.sh <tag> [steps]      steps: any of tests smoke bench bench2 trace
-# Outputs under gpurun_out/<tag>/.  Per-session variants (A/B builds, PMC
-# passes) go in git-ignored tools/_*.sh scripts.
+# Outputs under gpurun_out/<tag>/.  Per-session variants (A/B runs, PMC
+# passes) are tracked under tools/runs/<round>/, so every log a profiles/*/INDEX.md
+# cites can be regenerated from the repository.
 set -o pipefail
 TAG=${1:?tag}
 STEPS=${2:-"tests smoke bench"}
