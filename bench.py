@@ -451,32 +451,38 @@ def main():
                               "profiles/%s (a separate rocprofv3 --pmc run of the same build, on another box); "
                               "run_clock is this run's own" % PMC_PROFILE}
     run_ghz = (clk_before + clk_after) / 2
-    # the kernel's own clock relative to the probe's, both measured in one process (the PMC profile's
-    # GRBM clocks: profiles/r06/clock_probe_calibration_r06p.txt)
-    ratio = probe_ratio(pv, prof)
-    kclk = run_ghz * ratio if ratio else None
     roofline["run_clock"] = {"probe_ghz_before": round(clk_before, 3), "probe_ghz_after": round(clk_after, 3),
                              "probe_ghz": round(run_ghz, 3),
-                             "kernel_over_probe": round(ratio, 4) if ratio else None,
-                             "kernel_clock_est_ghz": round(kclk, 3) if kclk else None,
                              "note": "nt_dev_clock_probe right before and right after the one-stream timed region on "
                                      "its stream (ClockProbe): the shader clock this box holds under a verify-like "
-                                     "v_mad_u64_u32 load in this run; kernel_clock_est = probe x kernel_over_probe "
-                                     "(the two GRBM clocks of %s, one process)" % PMC_PROFILE}
+                                     "v_mad_u64_u32 load in this run"}
+    # The launch's cycle count does not depend on the box: GRBM_GUI_ACTIVE per 1M launch is 188.05 /
+    # 187.11 / 187.42 M in the r04 / r05 / r06 profiles (the same 5.33 G VALU).  So this run's kernel
+    # clock is that count over this run's launch time, and the r05 -> now comparison separates clock
+    # from code: equal cycles, different time = a different clock.
+    cyc_now = pv["per_launch"]["GRBM_GUI_ACTIVE"] / 8 if "GRBM_GUI_ACTIVE" in pvl else None
+    r05p = (load_profile(os.path.join("r05", "pmc_verify_sha.json")) or {}).get("kernels", {}).get("verify", {})
+    cyc_r05 = r05p["per_launch"]["GRBM_GUI_ACTIVE"] / 8 if "GRBM_GUI_ACTIVE" in r05p.get("per_launch", {}) else None
+    kclk = cyc_now / (kernel_ms * 1e-3) / 1e9 if cyc_now else None
+    roofline["kernel_clock"] = {"cycles_per_launch": round(cyc_now) if cyc_now else None,
+                                "implied_ghz": round(kclk, 3) if kclk else None,
+                                "implied_over_probe": round(kclk / run_ghz, 4) if kclk else None,
+                                "note": "cycles = GRBM_GUI_ACTIVE / 8 per 1M launch (%s, the same build; equal within "
+                                        "0.5 %% in the r04, r05 and r06 profiles); implied_ghz = those cycles / this "
+                                        "run's kernel_ms" % PMC_PROFILE}
     roofline["frac_at_run_clock"] = round(achieved / (MAD_PEAK_TS * (kclk or run_ghz) / 2.4), 4)
-    roofline["kernel_mcycles_at_run_clock"] = round(kernel_ms * (kclk or run_ghz) * 1e3, 1)
-    # round 5's driver run: 11.308 ms per 1M launch (BENCH_r05.json); its clock was not measured
-    # in that run -- the r05b PMC profile's effective clock of the same launch (another box) stands in
-    r05 = {"kernel_ms": 11.308, "clock_ghz": 1.979}
-    now_clk = kclk or run_ghz
-    roofline["vs_r05"] = {"kernel_ms_r05": r05["kernel_ms"], "kernel_ms": round(kernel_ms, 3),
-                          "time_ratio_r05_over_now": round(r05["kernel_ms"] / kernel_ms, 4),
-                          "clock_r05_ghz": r05["clock_ghz"], "clock_now_ghz": round(now_clk, 3),
-                          "cycle_ratio_r05_over_now": round(r05["kernel_ms"] * r05["clock_ghz"] / (kernel_ms * now_clk), 4),
-                          "note": "time_ratio > 1: this run's launch is faster; cycle_ratio normalises both by the "
-                                  "kernel's clock (r05: the GRBM clock of its PMC profile, no run clock existed; now: "
-                                  "this run's probe x kernel_over_probe) -- ~1 means the same instruction stream at a "
-                                  "different clock"}
+    # round 5's driver run: 11.308 ms per 1M launch (BENCH_r05.json); no clock was measured in that
+    # run -- its launch's cycle count (r05 profile, same instruction stream) gives its implied clock
+    r05_ms = 11.308
+    roofline["vs_r05"] = {"kernel_ms_r05": r05_ms, "kernel_ms": round(kernel_ms, 3),
+                          "time_ratio_r05_over_now": round(r05_ms / kernel_ms, 4),
+                          "cycles_r05": round(cyc_r05) if cyc_r05 else None,
+                          "cycles_now": round(cyc_now) if cyc_now else None,
+                          "cycle_ratio_r05_over_now": round(cyc_r05 / cyc_now, 4) if cyc_r05 and cyc_now else None,
+                          "implied_clock_r05_ghz": round(cyc_r05 / (r05_ms * 1e-3) / 1e9, 3) if cyc_r05 else None,
+                          "implied_clock_now_ghz": round(kclk, 3) if kclk else None,
+                          "note": "cycle_ratio ~1: the same code; time_ratio = the clock ratio of the two runs "
+                                  "(r05's driver box held ~2.07 GHz on this launch, this box implied_clock_now)"}
 
     # the other two halves of the metric, filled in when their configs have run, so
     # that they sit near the front of the line (a reader of its first few hundred
@@ -1438,9 +1444,12 @@ def keyset_roofline(launch_ms, step_ms, nsig, clk=None):
                           % PMC_KEYSET_PROFILE,
             **({"run_clock": {"probe_ghz_before": round(clk[0], 3), "probe_ghz_after": round(clk[1], 3),
                               "probe_ghz": round(sum(clk) / 2, 3),
-                              "kernel_over_probe": round(ratio, 4) if ratio else None,
-                              "kernel_clock_est_ghz": round(sum(clk) / 2 * ratio, 3) if ratio else None},
-                "frac_at_run_clock": round(achieved / (MAD_PEAK_TS * sum(clk) / 2 * (ratio or 1.0) / 2.4), 4)}
+                              "kernel_over_probe_pmc": round(ratio, 4) if ratio else None,
+                              "note": "the probe's clock around this run's key-cache region; kernel_over_probe_pmc = "
+                                      "the key-cache launch's GRBM clock / the probe's in one profiled process "
+                                      "(profiles/r06/clock_probe_calibration_r06p.txt): this kernel holds a lower "
+                                      "clock than the probe while it streams its random comb lines"},
+                "frac_at_run_clock": round(achieved / (MAD_PEAK_TS * sum(clk) / 2 / 2.4), 4)}
                if clk else {})}
 
 

@@ -1491,7 +1491,17 @@ static int keyset_create(nt_ctx* ctx, const uint8_t* pk32, uint32_t nkeys, int b
 extern "C" {
 
 int nt_keyset_create(nt_ctx* ctx, const uint8_t* pk32, uint32_t nkeys, nt_keyset** out) {
-  return keyset_create(ctx, pk32, nkeys, 0, out);
+  // the widest width that fits, or -- when hipMalloc refuses it (another process on the
+  // device may take the memory between the check and the allocation) -- the next narrower
+  const int b = keyset_comb_bits(ctx, nkeys);
+  if (b == 0 || std::getenv("NT_KEYSET_COMB_BITS")) return keyset_create(ctx, pk32, nkeys, b, out);
+  int rc = NT_ENOMEM;
+  for (const int w : {nt::kKeyCombReduced, nt::kKeyCombWide, nt::kKeyCombMid, nt::kKeyCombNarrow}) {
+    if (w > b) continue;
+    rc = keyset_create(ctx, pk32, nkeys, w, out);
+    if (rc != NT_ENOMEM) return rc;
+  }
+  return rc;
 }
 
 void nt_keyset_free(nt_keyset* ks) { delete ks; }

@@ -233,3 +233,51 @@ def test_registry_small_call_routing(reg):
         assert (h1 - h0, g1 - g0) == ((1, 0) if want_host else (0, 1)), (cpu, m)
     finally:
         reg.set_small_call_path(ntcrypto.NT_SMALL_OFF)
+
+
+def test_registry_concurrent_calls_during_admission(reg):
+    """Four threads call the plain entry points at once while the registry
+    admits the committee's keys on sight (the primary's tasks share one context):
+    every verdict is the expected one whichever snapshot a call ran with, and
+    by the end every decodable key is registered."""
+    import threading
+    rng = np.random.default_rng(15)
+    nk, G, q = 40, 64, 13
+    seeds = rng.integers(0, 256, (nk, 32), dtype=np.uint8)
+    pks = reg.sign_batch(seeds)
+    batches = []
+    for t in range(4):
+        digests = rng.integers(0, 256, (G, 32), dtype=np.uint8)
+        voters = np.concatenate([rng.permutation(nk)[:q] for _ in range(G)])
+        msg = digests[np.repeat(np.arange(G), q)].reshape(-1)
+        _, vsig = reg.sign_batch(seeds[voters], msg, np.arange(G * q, dtype=np.uint64) * 32,
+                                 np.full(G * q, 32, np.uint64))
+        vsig = vsig.copy()
+        bad = rng.random(G * q) < 0.05
+        vsig[bad, 5] ^= 1
+        want = ~bad.reshape(G, q).any(axis=1)
+        batches.append((pks[voters], vsig, digests, want))
+    first = np.arange(G, dtype=np.uint64) * q
+    cnt = np.full(G, q, np.uint32)
+    errors = []
+
+    def work(t):
+        try:
+            pk, sig, dg, want = batches[t]
+            for _ in range(12):
+                got = reg.verify_batch_groups(pk, sig, first, cnt, dg)
+                if not np.array_equal(got, want):
+                    errors.append((t, int((got != want).sum())))
+                reg.key_cache_info()
+        except Exception as e:  # surfaced below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    reg.key_cache_sync()
+    info = reg.key_cache_info()
+    assert info["keys"] == nk and info["error"] == 0 and info["hits"] > 0, info

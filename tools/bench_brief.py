@@ -47,4 +47,6 @@ def main(path):
 
 
 if __name__ == "__main__":
+    import signal
+    signal.signal(signal.SIGPIPE, signal.SIG_DFL)  # `| head` ends the summary quietly
     main(sys.argv[1])
