@@ -562,7 +562,8 @@ NT_D NT_INLINE uint32_t sort_bucket(uint32_t k, int mixed, uint32_t nkeys) {
 __global__ __launch_bounds__(kBlock) void k_key_hist(const uint32_t* __restrict__ key, uint64_t n, int mixed,
                                                     uint32_t nkeys, uint32_t* __restrict__ hist) {
   aux_priority();
-  __shared__ uint32_t h[kSortBuckets];
+  extern __shared__ uint32_t sort_lds[];  // nkeys + 1 counters (launch_verify_keyset sizes it)
+  uint32_t* h = sort_lds;
   for (uint32_t b = threadIdx.x; b <= nkeys; b += kBlock) h[b] = 0;
   __syncthreads();
   const uint64_t stride = (uint64_t)gridDim.x * kBlock * kHistTile;
@@ -590,10 +591,12 @@ __global__ __launch_bounds__(kBlock) void k_key_scatter(const uint32_t* __restri
                                                        uint32_t nkeys, uint32_t* __restrict__ lines,
                                                        uint32_t* __restrict__ perm) {
   aux_priority();
-  __shared__ uint32_t cnt[kSortBuckets];
-  __shared__ uint32_t base[kSortBuckets];
-  __shared__ uint32_t part[kBlock];
-  const uint32_t nb = nkeys + 1, per = (nb + kBlock - 1) / kBlock, b0 = threadIdx.x * per;
+  extern __shared__ uint32_t sort_lds[];  // cnt[nkeys + 1], base[nkeys + 1], part[kBlock]
+  const uint32_t nb = nkeys + 1;
+  uint32_t* cnt = sort_lds;
+  uint32_t* base = sort_lds + nb;
+  uint32_t* part = sort_lds + 2 * nb;
+  const uint32_t per = (nb + kBlock - 1) / kBlock, b0 = threadIdx.x * per;
   uint32_t sum = 0;
   for (uint32_t b = b0; b < b0 + per && b < nb; ++b) sum += lines[b * kCtrStride];
   part[threadIdx.x] = sum;
@@ -693,12 +696,15 @@ __global__ __launch_bounds__(kBlock) void k_ks_init(uint32_t* __restrict__ ctr, 
   const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x, stride = (uint64_t)gridDim.x * kBlock;
   for (uint64_t i = t; i < nctr; i += stride) ctr[i] = 0u;
   for (uint64_t i = t; i < nsw; i += stride) sw[i] = 0ull;
-  const uint64_t ngw = (G + 63) / 64;
-  for (uint64_t w = t; w < ngw; w += stride) {
-    unsigned long long v = G - 64 * w >= 64 ? ~0ull : (1ull << (G - 64 * w)) - 1ull;
-    for (uint64_t g = 64 * w; g < G && g < 64 * w + 64; ++g)
-      if (gfirst[g] + gcnt[g] > n) v &= ~(1ull << (g & 63));
-    gw[w] = v;
+  // one lane per group, one ballot per word (a wave's 64 lanes are one word:
+  // kBlock and the stride are multiples of 64, so the loop is wave-uniform).
+  // Round 6's first version looped over a word's 64 groups in one lane: 64
+  // loads in a row, 60-80 us per launch beside a key-cache launch (r06p trace).
+  const uint64_t ng = (G + 63) / 64 * 64;
+  for (uint64_t g = t; g < ng; g += stride) {
+    const bool ok = g < G && gfirst[g] + gcnt[g] <= n;
+    const unsigned long long bal = __ballot(ok);
+    if ((threadIdx.x & 63u) == 0) gw[g >> 6] = bal;
   }
 }
 
@@ -734,7 +740,7 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
     const uint64_t gi = fuse && lo == 0 ? G : 0;  // group words: set once, by the first launch's init
     const uint32_t nctr = sorted ? (uint32_t)((kSortHdr + 4ull * kCtrStride * (nkeys + 1)) / 4) : 1u;
     const uint64_t nsw = sorted && fuse ? (m + 63) / 64 : 0;
-    const uint64_t most = std::max<uint64_t>(std::max<uint64_t>(nctr, nsw), (gi + 63) / 64);
+    const uint64_t most = std::max<uint64_t>(std::max<uint64_t>(nctr, nsw), (gi + 63) / 64 * 64);
     const uint32_t ib = (uint32_t)std::min<uint64_t>(1024, (most + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_ks_init, dim3(ib ? ib : 1), dim3(kBlock), 0, s, ctr, nctr,
                        (unsigned long long*)(d_out_words + lo / 64), nsw, d_gfirst, d_gcnt, gi, n,
@@ -747,10 +753,15 @@ hipError_t launch_verify_keyset(int mode, int key_bits, const uint32_t* d_key_id
       // LDS histogram with one global atomic per bucket)
       const uint64_t hw = (m + (uint64_t)kBlock * kHistTile - 1) / ((uint64_t)kBlock * kHistTile);
       const uint32_t hb = (uint32_t)(hw < 512 ? hw : 512);
-      hipLaunchKernelGGL(k_key_hist, dim3(hb), dim3(kBlock), 0, s, d_key_idx + lo, m, mixed, nkeys, hist);
+      // LDS sized to the committee (nkeys + 1 buckets), not to kSortBuckets: a
+      // 101-key committee's scatter block takes 1.8 KB instead of 33 KB, so it
+      // finds room on a CU beside the other stream's key-cache launch
+      // (profiles/r06/shard8_trace_r06p.txt: the 33 KB blocks waited ~0.7 ms)
+      const size_t hist_lds = 4ull * (nkeys + 1), scat_lds = 4ull * (2ull * (nkeys + 1) + kBlock);
+      hipLaunchKernelGGL(k_key_hist, dim3(hb), dim3(kBlock), hist_lds, s, d_key_idx + lo, m, mixed, nkeys, hist);
       const uint64_t sb = (m + (uint64_t)kBlock * kSortTile - 1) / ((uint64_t)kBlock * kSortTile);
-      hipLaunchKernelGGL(k_key_scatter, dim3((uint32_t)sb), dim3(kBlock), 0, s, d_key_idx + lo, m, mixed, nkeys, hist,
-                         p);
+      hipLaunchKernelGGL(k_key_scatter, dim3((uint32_t)sb), dim3(kBlock), scat_lds, s, d_key_idx + lo, m, mixed, nkeys,
+                         hist, p);
       if ((e = hipGetLastError()) != hipSuccess) return e;
       perm = p;
     }
