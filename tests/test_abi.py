@@ -22,7 +22,7 @@ def _declared():
 @pytest.fixture(scope="module")
 def lib():
     if not os.path.exists(LIB):
-        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "narwhal-tusk_amd")], check=True)
+        subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "narwhal-tusk_amd")], check=True)
     return ctypes.CDLL(LIB)
 
 

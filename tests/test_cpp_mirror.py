@@ -12,7 +12,7 @@ CPP = os.path.join(ROOT, "tests", "cpp")
 
 
 def _build():
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "narwhal-tusk_amd")], check=True)
+    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "narwhal-tusk_amd")], check=True)
     subprocess.run(["make", "-s", "-C", CPP, "build/test_narwhal"], check=True)
     return os.path.join(CPP, "build", "test_narwhal")
 
