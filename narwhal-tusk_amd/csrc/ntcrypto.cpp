@@ -32,6 +32,25 @@
 
 namespace ntrt {
 
+// NT_TABLE_ALLOC=contig (A/B): comb tables from physically contiguous VRAM
+// (hipExtMallocWithFlags + hipDeviceMallocContiguous; hipMalloc when that is
+// refused), to see whether the key-cache kernel's random comb lines pay for
+// address translation beyond what the driver's own placement gives
+hipError_t table_malloc(void** p, size_t bytes) {
+  static const bool contig = [] {
+    const char* e = std::getenv("NT_TABLE_ALLOC");
+    return e && std::strcmp(e, "contig") == 0;
+  }();
+  if (contig) {
+    const hipError_t e = hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous);
+    if (std::getenv("NT_REG_TRACE"))
+      std::fprintf(stderr, "[alloc] contiguous %.2f GB: %s\n", bytes / 1e9, e == hipSuccess ? "ok" : "refused");
+    if (e == hipSuccess) return e;
+    (void)hipGetLastError();
+  }
+  return hipMalloc(p, bytes);
+}
+
 // nt_host_alloc registry (runtime.hpp)
 std::mutex g_pin_mu;
 std::map<uintptr_t, uint64_t> g_pinned;
@@ -60,7 +79,7 @@ std::shared_ptr<CombB> shared_comb_b(Device& dv, int bits, int& rc) {
     rc = NT_EHIP;
     return nullptr;
   }
-  if (hipMalloc(&c->p, nt::wcomb_bytes_per_key(bits)) != hipSuccess) {
+  if (table_malloc((void**)&c->p, nt::wcomb_bytes_per_key(bits)) != hipSuccess) {
     (void)hipGetLastError();  // an out-of-memory hipMalloc leaves no sticky error: clear it
     c->p = nullptr;
     rc = NT_ENOMEM;
@@ -1469,7 +1488,7 @@ static int keyset_create(nt_ctx* ctx, const uint8_t* pk32, uint32_t nkeys, int b
     pd.reserved = comb;
     if (hipMalloc(&pd.d_enc, 32 * nk) != hipSuccess) return NT_ENOMEM;
     if (hipMalloc(&pd.d_meta, 4 * nk) != hipSuccess) return NT_ENOMEM;
-    if (hipMalloc(&pd.d_comb, comb) != hipSuccess) {
+    if (table_malloc((void**)&pd.d_comb, comb) != hipSuccess) {
       (void)hipGetLastError();
       pd.d_comb = nullptr;
       return NT_ENOMEM;

@@ -107,7 +107,7 @@ struct KeyReg {
       pd.budget = dv.budget;
       pd.reserved = comb;
       if (hipMalloc(&pd.d_enc, 32ull * cap) != hipSuccess || hipMalloc(&pd.d_meta, 4ull * cap) != hipSuccess ||
-          hipMalloc(&pd.d_comb, comb) != hipSuccess) {
+          table_malloc((void**)&pd.d_comb, comb) != hipSuccess) {
         (void)hipGetLastError();
         return NT_ENOMEM;
       }

@@ -480,6 +480,7 @@ void reg_note_misses(nt_ctx* ctx, const std::vector<const uint8_t*>& keys);
 void reg_count(nt_ctx* ctx, uint64_t hits, uint64_t misses);
 // first-use tables and width choice shared with nt_keyset_create (ntcrypto.cpp)
 int keyset_comb_bits(nt_ctx* ctx, uint32_t nkeys);
+hipError_t table_malloc(void** p, size_t bytes);  // comb tables (NT_TABLE_ALLOC)
 int comb_b_for(Device& dv);
 
 }  // namespace ntrt
